@@ -1,0 +1,172 @@
+/*
+ * lsmbloom.h — C ABI of the MI355X-native Bloom-filter engine.
+ *
+ * Drop-in boundary for G1DO/Storage-Engine `src/bloom` (Rust).  The store's
+ * callers — SSTableBuilder (src/sstable/builder.rs:74,93,177-182), SSTable::open
+ * (src/sstable/reader.rs:78-82), SSTable::get (src/sstable/reader.rs:197) — keep
+ * calling the Rust surface `crate::bloom::{BloomFilter, BloomFilterBuilder}`;
+ * a thin Rust shim forwards to the entry points below.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; all buffers are caller-owned and the
+ *     library keeps no pointer after a call returns.
+ *   - Return 0 (LSMB_OK) on success, a negative LSMB_E* code otherwise; the
+ *     thread-local message of the last failure is lsmb_last_error().
+ *   - Where the reference panics (assert!/division by zero), the ABI returns
+ *     LSMB_EINVAL; where it returns Err(Error::Corruption) (deserialize), the
+ *     ABI returns LSMB_ECORRUPT (src/error.rs:12).
+ *   - Filter words are the reference's `bits: Vec<u64>` (src/bloom/mod.rs:24):
+ *     ceil(num_bits/64) little-endian u64, bit p = word p/64, bit p%64.
+ *   - Batched build entry points OR-ACCUMULATE into `words` (existing bits are
+ *     kept), so a build after insert()s, or a merge of shard partials, is exact.
+ *   - Batched entry points run on the GPU only.  With no usable gfx950 device,
+ *     lsmb_open fails with LSMB_ENODEV: there is no silent CPU fallback.
+ *   - Thread safety: a context may be used from one thread at a time; distinct
+ *     contexts (e.g. flush + background compaction, src/compaction/scheduler.rs:37)
+ *     may run concurrently.  Stateless functions are always thread safe.
+ */
+#ifndef LSMBLOOM_H
+#define LSMBLOOM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LSMB_OK 0
+#define LSMB_EINVAL (-1)   /* argument the reference rejects by panicking      */
+#define LSMB_ENODEV (-2)   /* no gfx950 device / HIP initialisation failed     */
+#define LSMB_EHIP (-3)     /* HIP runtime or kernel launch error               */
+#define LSMB_ECORRUPT (-4) /* serialized filter fails validation               */
+#define LSMB_ENOMEM (-5)   /* device or pinned-host allocation failed          */
+
+#define LSMB_ABI_VERSION 1
+
+typedef struct lsmb_ctx lsmb_ctx; /* one GPU: stream, events, scratch arenas */
+
+int lsmb_abi_version(void);
+const char* lsmb_last_error(void);
+
+/* ---- sizing ------------------------------------------------------------ */
+
+/* BloomFilter::new(expected_items, false_positive_rate) sizing
+ * (src/bloom/mod.rs:38-67): num_bits = max(sat_u32(ceil(n * -1.44*log2 fpr)), 64),
+ * num_hashes = max(ceil(bpk * ln 2), 1).  LSMB_EINVAL where the reference
+ * panics (n == 0, fpr outside (0,1); :39-43). */
+int lsmb_params(uint64_t expected_items, double false_positive_rate, uint32_t* num_bits,
+                uint32_t* num_hashes);
+
+/* ceil(num_bits / 64): length of the words array (src/bloom/mod.rs:58). */
+uint64_t lsmb_num_words(uint32_t num_bits);
+
+/* ---- format (src/bloom/mod.rs:102-168) --------------------------------- */
+
+/* 12 + 8 * ceil(num_bits/64)  (serialize, :102-115). */
+uint64_t lsmb_serialized_size(uint32_t num_bits);
+
+/* BloomFilter::serialize (:102-115): [num_hashes u32][num_bits u32]
+ * [num_u64s u32][words u64...] little-endian.  out_len must be >= the size. */
+int lsmb_serialize(const uint64_t* words, uint32_t num_bits, uint32_t num_hashes, uint8_t* out,
+                   uint64_t out_len);
+
+/* BloomFilter::deserialize validation (:123-153): len >= 12, num_u64s ==
+ * ceil(num_bits/64), len == 12 + 8*num_u64s; else LSMB_ECORRUPT. */
+int lsmb_deserialize_header(const uint8_t* data, uint64_t len, uint32_t* num_hashes,
+                            uint32_t* num_bits, uint32_t* num_u64s);
+
+/* Validates like lsmb_deserialize_header, then copies the words (:156-161). */
+int lsmb_deserialize(const uint8_t* data, uint64_t len, uint64_t* words, uint64_t words_cap);
+
+/* ---- single-key operations (BloomFilter::insert / may_contain) ---------- */
+
+/* BloomFilter::insert (src/bloom/mod.rs:70-78) on host-resident words: one
+ * key, so no device round trip (a launch costs ~10 us, the insert ~20 ns). */
+int lsmb_insert(uint64_t* words, uint32_t num_bits, uint32_t num_hashes, const uint8_t* key,
+                uint64_t key_len);
+
+/* BloomFilter::may_contain (:82-94).  Returns 1 / 0, or < 0 on error. */
+int lsmb_may_contain(const uint64_t* words, uint32_t num_bits, uint32_t num_hashes,
+                     const uint8_t* key, uint64_t key_len);
+
+/* Debug/test helper: the k bit positions of one key (hash_key + get_position,
+ * src/bloom/mod.rs:181-197). */
+int lsmb_positions(const uint8_t* key, uint64_t key_len, uint32_t num_bits, uint32_t num_hashes,
+                   uint32_t* out_positions);
+
+/* ---- GPU context --------------------------------------------------------- */
+
+/* Opens `device` (HIP ordinal; -1 = current device).  LSMB_ENODEV if no
+ * gfx950 device is usable. */
+int lsmb_open(lsmb_ctx** out, int device);
+void lsmb_close(lsmb_ctx* ctx);
+
+/* Blocks until all work issued on the context's stream has finished. */
+int lsmb_sync(lsmb_ctx* ctx);
+
+/* ---- batched build (BloomFilterBuilder::add_key loop + build) ------------ */
+/* Host-memory entry points: H2D the keys through pinned staging, build on the
+ * GPU, D2H the words (OR-accumulated into `words`).  Synchronous. */
+
+/* n keys of key_len bytes each, packed back to back (key i at keys + i*key_len). */
+int lsmb_build_fixed(lsmb_ctx* ctx, const uint8_t* keys, uint32_t key_len, uint64_t n,
+                     uint32_t num_bits, uint32_t num_hashes, uint64_t* words);
+
+/* n variable-length keys: key i = data[offsets[i] .. offsets[i+1]). */
+int lsmb_build_var(lsmb_ctx* ctx, const uint8_t* data, const uint64_t* offsets, uint64_t n,
+                   uint32_t num_bits, uint32_t num_hashes, uint64_t* words);
+
+/* ---- batched probe (may_contain over a batch of keys x filters) --------- */
+/* For key i and filter f: bit (f % 8) of out_mask[i * ceil(nfilt/8) + f / 8]
+ * = may_contain(filter f, key i), exactly what SSTable::get's bloom check
+ * (src/sstable/reader.rs:197) answers for that SSTable.  offsets == NULL
+ * selects fixed-length keys of key_len bytes.  nfilt <= 64. */
+int lsmb_probe(lsmb_ctx* ctx, const uint64_t* const* filt_words, const uint32_t* filt_bits,
+               const uint32_t* filt_hashes, uint32_t nfilt, const uint8_t* data,
+               const uint64_t* offsets, uint32_t key_len, uint64_t n, uint8_t* out_mask);
+
+/* ---- device-resident entry points ---------------------------------------- */
+/* All pointers are device pointers (hipMalloc).  `stream` is a hipStream_t
+ * (NULL = the context's own stream).  Asynchronous: the call returns after
+ * enqueueing; synchronise on the stream before reading results. */
+
+int lsmb_build_fixed_dev(lsmb_ctx* ctx, const void* d_keys, uint32_t key_len, uint64_t n,
+                         uint32_t num_bits, uint32_t num_hashes, void* d_words, void* stream);
+
+int lsmb_build_var_dev(lsmb_ctx* ctx, const void* d_data, const void* d_offsets, uint64_t n,
+                       uint32_t num_bits, uint32_t num_hashes, void* d_words, void* stream);
+
+/* d_filt_words: host array of nfilt DEVICE pointers. */
+int lsmb_probe_dev(lsmb_ctx* ctx, const void* const* d_filt_words, const uint32_t* filt_bits,
+                   const uint32_t* filt_hashes, uint32_t nfilt, const void* d_data,
+                   const void* d_offsets, uint32_t key_len, uint64_t n, void* d_out_mask,
+                   void* stream);
+
+/* OR-reduce: d_dst[i] |= d_src[j*stride_words + i] for j < nsrc, i < nwords.
+ * The merge step of a sharded build (partial filters -> one filter). */
+int lsmb_or_reduce_dev(lsmb_ctx* ctx, void* d_dst, const void* d_src, uint64_t nwords,
+                       uint32_t nsrc, uint64_t stride_words, void* stream);
+
+/* Synthetic workload generators, device-side:
+ * key16(seed, i) = LE64(splitmix64(seed+2i)) || LE64(splitmix64(seed+2i+1)),
+ * for i in [first, first+n). */
+int lsmb_gen_key16_dev(lsmb_ctx* ctx, uint64_t seed, uint64_t first, uint64_t n, void* d_keys,
+                       void* stream);
+
+/* ---- introspection ------------------------------------------------------- */
+
+/* Name of the build strategy the dispatcher picks for (num_bits, n), e.g.
+ * "lds", "partition", "atomic" (for tests and bench reporting). */
+const char* lsmb_build_strategy(uint32_t num_bits, uint64_t n);
+
+/* Timing of the last device build on this context, in milliseconds, per phase
+ * (HIP events on the build stream): [0] total, [1] pass A (hash + bin),
+ * [2] pass B (apply).  Valid after lsmb_sync. */
+int lsmb_last_build_ms(lsmb_ctx* ctx, float* out3);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LSMBLOOM_H */

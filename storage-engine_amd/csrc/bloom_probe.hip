@@ -1,0 +1,153 @@
+// bloom_probe.hip — batched multi-filter probe kernels for gfx950 (MI355X).
+//
+// Answers, for a batch of Q keys and F filters, exactly what the reference's
+// per-SSTable check `bloom.may_contain(key)` (src/sstable/reader.rs:197 ->
+// src/bloom/mod.rs:82-94) answers for each (key, filter) pair; DB::get walks
+// L0 newest-first then L1+ and calls it once per SSTable (src/db/mod.rs:243-267).
+// Each key is hashed ONCE (XXH3-128) whatever F is.
+//
+//   k_probe_sliced   all F filters share (num_bits, k) — the store's SSTable
+//                    filters do: SSTableBuilder::new always sizes new(1000, 0.01)
+//                    (src/sstable/builder.rs:51,74), 9 568 bits, k = 7.  Each
+//                    workgroup bit-slices the F filters into one LDS table
+//                    (entry p = the F filters' bit p), so a key costs k LDS
+//                    reads and one AND chain for all F filters at once.
+//   k_probe_generic  any mix of filters: per filter an exact position walk,
+//                    bits read from HBM/L2 with early exit (mod.rs:88-90; the
+//                    answer does not depend on early exit).
+//
+// Output row i (ceil(F/8) bytes): bit f%8 of byte f/8 = may_contain(f, key i).
+#include "kernels.hpp"
+#include "keysrc.hpp"
+
+namespace lsmb {
+namespace {
+
+using ks::Fixed16;
+using ks::FixedN;
+using ks::VarLen;
+
+template <typename T>
+__device__ __forceinline__ void store_row(uint8_t* out, uint64_t i, uint32_t stride, T m) {
+    if (sizeof(T) == 1) {
+        out[i] = (uint8_t)m;
+    } else if (stride == sizeof(T)) {
+        reinterpret_cast<T*>(out)[i] = m;
+    } else {
+        for (uint32_t s = 0; s < stride; s++) out[i * stride + s] = (uint8_t)(m >> (8 * s));
+    }
+}
+
+// T holds up to 8*sizeof(T) filters' bits per position.
+template <class Src, typename T>
+__global__ __launch_bounds__(256) void k_probe_sliced(Src src, uint64_t n, Mod32 md, uint32_t k,
+                                                      uint32_t num_bits,
+                                                      const ProbeFilter* __restrict__ filters,
+                                                      uint32_t nfilt, uint32_t stride,
+                                                      uint8_t* __restrict__ out) {
+    extern __shared__ __align__(16) uint8_t smem_raw[];
+    T* table = reinterpret_cast<T*>(smem_raw);
+    const uint32_t nw32 = (num_bits + 31) / 32;
+    for (uint32_t w = threadIdx.x; w < nw32; w += blockDim.x) {
+        T acc[32];
+#pragma unroll
+        for (int b = 0; b < 32; b++) acc[b] = 0;
+        for (uint32_t f = 0; f < nfilt; f++) {
+            const uint32_t x = filters[f].words32[w];
+            const uint32_t ob = filters[f].out_bit;
+#pragma unroll
+            for (int b = 0; b < 32; b++) acc[b] |= (T)((T)((x >> b) & 1u) << ob);
+        }
+#pragma unroll
+        for (int b = 0; b < 32; b++) table[w * 32 + b] = acc[b];
+    }
+    __syncthreads();
+    T all = 0;
+    for (uint32_t f = 0; f < nfilt; f++) all |= (T)((T)1 << filters[f].out_bit);
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
+        H128 h = src.hash(i);
+        PosWalk pw(md, h.lo, h.hi);
+        T m = all;
+        for (uint32_t j = 0; j < k; j++) {
+            m &= table[pw.pos()];
+            pw.next(md);
+        }
+        store_row<T>(out, i, stride, m);
+    }
+}
+
+template <class Src>
+__global__ __launch_bounds__(256) void k_probe_generic(Src src, uint64_t n,
+                                                       const ProbeFilter* __restrict__ filters,
+                                                       uint32_t nfilt, uint32_t stride,
+                                                       uint8_t* __restrict__ out) {
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
+        H128 h = src.hash(i);
+        uint64_t m = 0;
+        for (uint32_t f = 0; f < nfilt; f++) {
+            const ProbeFilter& F = filters[f];
+            bool hit = true;
+            if (F.k) {
+                PosWalk pw(F.md, h.lo, h.hi);
+                for (uint32_t j = 0; j < F.k; j++) {
+                    const uint32_t p = pw.pos();
+                    if (!((F.words32[p >> 5] >> (p & 31)) & 1u)) {
+                        hit = false;
+                        break;
+                    }
+                    pw.next(F.md);
+                }
+            }
+            if (hit) m |= 1ull << F.out_bit;
+        }
+        for (uint32_t s = 0; s < stride; s++) out[i * stride + s] = (uint8_t)(m >> (8 * s));
+    }
+}
+
+template <class Src>
+hipError_t probe_with(const Src& src, uint64_t n, const ProbeFilter* hf, uint32_t nfilt,
+                      const ProbeFilter* df, uint8_t* out, int num_cus, hipStream_t st) {
+    const uint32_t stride = (nfilt + 7) / 8;
+    bool same = nfilt > 0 && hf[0].k > 0;
+    for (uint32_t f = 1; f < nfilt && same; f++)
+        same = hf[f].num_bits == hf[0].num_bits && hf[f].k == hf[0].k;
+    uint64_t g = (n + 255) / 256;
+    const uint64_t gmax = (uint64_t)num_cus * 8;
+    if (g > gmax) g = gmax;
+    if (g < 1) g = 1;
+    if (same && nfilt <= 32) {
+        const uint32_t nb = hf[0].num_bits;
+        const size_t ent = (size_t)((nb + 31) / 32) * 32;
+        const size_t tsz = nfilt <= 8 ? 1 : nfilt <= 16 ? 2 : 4;
+        const size_t smem = ent * tsz;
+        if (smem <= 64 * 1024) {
+            auto go = [&](auto kern) {
+                hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+                kern<<<dim3((uint32_t)g), dim3(256), smem, st>>>(src, n, hf[0].md, hf[0].k, nb, df, nfilt,
+                                                                 stride, out);
+            };
+            if (tsz == 1) go(k_probe_sliced<Src, uint8_t>);
+            else if (tsz == 2) go(k_probe_sliced<Src, uint16_t>);
+            else go(k_probe_sliced<Src, uint32_t>);
+            return hipGetLastError();
+        }
+    }
+    k_probe_generic<Src><<<dim3((uint32_t)g), dim3(256), 0, st>>>(src, n, df, nfilt, stride, out);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_probe(const KeyBatch& kb, const ProbeFilter* hf, uint32_t nfilt,
+                        ProbeFilter* df, uint8_t* out, int num_cus, hipStream_t st) {
+    if (kb.n == 0) return hipSuccess;
+    if (kb.offsets) return probe_with(VarLen{kb.data, kb.offsets}, kb.n, hf, nfilt, df, out, num_cus, st);
+    if (kb.key_len == 16 && (reinterpret_cast<uintptr_t>(kb.data) & 15) == 0)
+        return probe_with(Fixed16{reinterpret_cast<const uint4*>(kb.data)}, kb.n, hf, nfilt, df, out,
+                          num_cus, st);
+    return probe_with(FixedN{kb.data, kb.key_len}, kb.n, hf, nfilt, df, out, num_cus, st);
+}
+
+}  // namespace lsmb

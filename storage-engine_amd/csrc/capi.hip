@@ -1,0 +1,546 @@
+// capi.hip — the C ABI (include/lsmbloom.h) over the HIP kernels.
+//
+// Host-side plumbing only: argument validation with the reference's error
+// behaviour, the per-GPU context (stream, events, grow-only device arenas),
+// chunking of large builds, and the format functions of src/bloom/mod.rs.
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/lsmbloom.h"
+#include "kernels.hpp"
+
+using namespace lsmb;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    return fail(LSMB_EHIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr)                                   \
+    do {                                                \
+        hipError_t e_ = (expr);                         \
+        if (e_ != hipSuccess) return hip_fail(e_, #expr); \
+    } while (0)
+
+uint64_t nwords64(uint32_t num_bits) { return ((uint64_t)num_bits + 63) / 64; }
+
+uint32_t rd32le(const uint8_t* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// Reference arguments that would panic (% by zero in get_position, mod.rs:195).
+int check_filter(uint32_t num_bits, uint32_t k) {
+    if (num_bits == 0 && k > 0)
+        return fail(LSMB_EINVAL, "num_bits == 0 with num_hashes > 0 (reference panics: %% by zero)");
+    return LSMB_OK;
+}
+
+// A grow-only device buffer.
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t want) {
+        if (want <= bytes) return hipSuccess;
+        if (p) hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) bytes = want;
+        return e;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+};
+
+uint64_t workspace_limit_entries() {
+    const char* s = getenv("LSMB_WORKSPACE_MB");
+    uint64_t mb = s ? strtoull(s, nullptr, 10) : 8192;
+    if (mb < 16) mb = 16;
+    return mb * (1ull << 20) / 4;
+}
+
+}  // namespace
+
+struct lsmb_ctx {
+    int dev = 0;
+    int num_cus = 256;
+    hipStream_t st = nullptr;
+    BuildTimers tm;
+    DevBuf ws_bins, ws_cursor;     // partition workspace
+    DevBuf keys, offs, words, out; // staging for the host-memory entry points
+    DevBuf filt_words;             // probe: device copies of host filters
+    DevBuf filt_desc;              // probe: ProbeFilter array
+    std::vector<ProbeFilter> hfilt;
+    std::vector<ProbeFilter> desc_uploaded;  // what filt_desc currently holds
+    ProbeFilter* desc_pinned = nullptr;      // pinned staging for descriptor uploads
+    hipEvent_t desc_done = nullptr;          // last kernel that read filt_desc
+    std::vector<uint64_t> offs_tmp;
+};
+
+namespace {
+
+struct DevGuard {
+    int prev = -1;
+    explicit DevGuard(int dev) {
+        hipGetDevice(&prev);
+        if (prev != dev) hipSetDevice(dev);
+    }
+    ~DevGuard() {
+        int cur = -1;
+        hipGetDevice(&cur);
+        if (prev >= 0 && cur != prev) hipSetDevice(prev);
+    }
+};
+
+hipStream_t pick_stream(lsmb_ctx* c, void* stream) {
+    return stream ? reinterpret_cast<hipStream_t>(stream) : c->st;
+}
+
+// Device build of one batch, chunked so the partition workspace stays bounded.
+int build_dev(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k, uint32_t* dw,
+              hipStream_t st) {
+    const BuildStrategy s = pick_build_strategy(num_bits, k, kb_all.n);
+    c->tm.valid = false;
+    if (s == BuildStrategy::None) return LSMB_OK;
+    if (s != BuildStrategy::Partition) {
+        HIP_TRY(launch_build(kb_all, num_bits, k, dw, s, PartitionWorkspace{}, c->num_cus, st, &c->tm));
+        return LSMB_OK;
+    }
+    const uint64_t limit = workspace_limit_entries();
+    uint64_t chunk = partition_chunk_keys(num_bits, k, limit);
+    if (chunk == 0) return fail(LSMB_ENOMEM, "partition workspace limit too small");
+    chunk = std::min(chunk, kb_all.n);
+    uint32_t nbins, cap;
+    partition_sizing(num_bits, k, chunk, &nbins, &cap);
+    HIP_TRY(c->ws_bins.ensure((size_t)nbins * cap * 4));
+    HIP_TRY(c->ws_cursor.ensure((size_t)nbins * 4));
+    PartitionWorkspace ws;
+    ws.bins = (uint32_t*)c->ws_bins.p;
+    ws.cursor = (uint32_t*)c->ws_cursor.p;
+    ws.entries = c->ws_bins.bytes / 4;
+    ws.nbins_cap = (uint32_t)(c->ws_cursor.bytes / 4);
+    for (uint64_t first = 0; first < kb_all.n; first += chunk) {
+        KeyBatch kb = kb_all;
+        kb.n = std::min(chunk, kb_all.n - first);
+        if (kb.offsets)
+            kb.offsets += first;  // VarLen offsets are absolute into data
+        else
+            kb.data += first * kb.key_len;
+        HIP_TRY(launch_build(kb, num_bits, k, dw, s, ws, c->num_cus, st, &c->tm));
+    }
+    return LSMB_OK;
+}
+
+}  // namespace
+
+namespace lsmb {
+
+bool bloom_params(uint64_t n, double fpr, uint32_t* num_bits, uint32_t* num_hashes) {
+    if (n == 0 || !(fpr > 0.0 && fpr < 1.0)) return false;
+    auto sat = [](double x) -> uint32_t {  // Rust `f64 as u32` saturates
+        if (!(x == x) || x <= 0.0) return 0;
+        if (x >= 4294967295.0) return 4294967295u;
+        return (uint32_t)x;
+    };
+    const double bpk = -1.44 * log2(fpr);                      // mod.rs:46
+    uint32_t nb = sat(ceil((double)n * bpk));                   // mod.rs:49
+    if (nb < 64) nb = 64;                                       // mod.rs:52
+    uint32_t k = sat(ceil(bpk * log(2.0)));                     // mod.rs:55
+    if (k < 1) k = 1;                                           // mod.rs:56
+    *num_bits = nb;
+    *num_hashes = k;
+    return true;
+}
+
+}  // namespace lsmb
+
+extern "C" {
+
+int lsmb_abi_version(void) { return LSMB_ABI_VERSION; }
+const char* lsmb_last_error(void) { return g_err.c_str(); }
+
+int lsmb_params(uint64_t n, double fpr, uint32_t* num_bits, uint32_t* num_hashes) {
+    if (!num_bits || !num_hashes) return fail(LSMB_EINVAL, "null output pointer");
+    if (n == 0) return fail(LSMB_EINVAL, "expected_items must be > 0");
+    if (!bloom_params(n, fpr, num_bits, num_hashes)) return fail(LSMB_EINVAL, "FPR must be in (0, 1)");
+    return LSMB_OK;
+}
+
+uint64_t lsmb_num_words(uint32_t num_bits) { return nwords64(num_bits); }
+uint64_t lsmb_serialized_size(uint32_t num_bits) { return 12 + 8 * nwords64(num_bits); }
+
+int lsmb_serialize(const uint64_t* words, uint32_t num_bits, uint32_t k, uint8_t* out, uint64_t out_len) {
+    const uint64_t nw = nwords64(num_bits);
+    if (out_len < 12 + 8 * nw) return fail(LSMB_EINVAL, "serialize: output buffer too small");
+    if (nw && !words) return fail(LSMB_EINVAL, "serialize: null words");
+    const uint32_t hdr[3] = {k, num_bits, (uint32_t)nw};
+    for (int j = 0; j < 3; j++)
+        for (int b = 0; b < 4; b++) out[4 * j + b] = (uint8_t)(hdr[j] >> (8 * b));
+    // words are little-endian u64 on this (x86-64) host: a straight copy.
+    if (nw) memcpy(out + 12, words, 8 * nw);
+    return LSMB_OK;
+}
+
+int lsmb_deserialize_header(const uint8_t* data, uint64_t len, uint32_t* k, uint32_t* num_bits,
+                            uint32_t* num_u64s) {
+    if (len < 12 || !data) return fail(LSMB_ECORRUPT, "bloom filter too short for header");
+    const uint32_t nh = rd32le(data), nb = rd32le(data + 4), nw = rd32le(data + 8);
+    const uint64_t expect = nwords64(nb);
+    if ((uint64_t)nw != expect)
+        return fail(LSMB_ECORRUPT, "bloom filter num_u64s mismatch: got %u, expected %llu", nw,
+                    (unsigned long long)expect);
+    const uint64_t want = 12 + 8 * (uint64_t)nw;
+    if (len != want)
+        return fail(LSMB_ECORRUPT, "bloom filter data length mismatch: got %llu, expected %llu",
+                    (unsigned long long)len, (unsigned long long)want);
+    if (k) *k = nh;
+    if (num_bits) *num_bits = nb;
+    if (num_u64s) *num_u64s = nw;
+    return LSMB_OK;
+}
+
+int lsmb_deserialize(const uint8_t* data, uint64_t len, uint64_t* words, uint64_t cap) {
+    uint32_t k, nb, nw;
+    int rc = lsmb_deserialize_header(data, len, &k, &nb, &nw);
+    if (rc) return rc;
+    if (cap < nw) return fail(LSMB_EINVAL, "deserialize: words buffer too small");
+    if (nw) memcpy(words, data + 12, 8 * (uint64_t)nw);
+    return LSMB_OK;
+}
+
+int lsmb_positions(const uint8_t* key, uint64_t len, uint32_t num_bits, uint32_t k, uint32_t* out) {
+    if (int rc = check_filter(num_bits, k)) return rc;
+    if (!k) return LSMB_OK;
+    const Mod32 md = Mod32::make(num_bits);
+    const H128 h = xxh3_128(key, len);
+    PosWalk pw(md, h.lo, h.hi);
+    for (uint32_t i = 0; i < k; i++) {
+        out[i] = pw.pos();
+        pw.next(md);
+    }
+    return LSMB_OK;
+}
+
+int lsmb_insert(uint64_t* words, uint32_t num_bits, uint32_t k, const uint8_t* key, uint64_t len) {
+    if (int rc = check_filter(num_bits, k)) return rc;
+    if (!k) return LSMB_OK;
+    const Mod32 md = Mod32::make(num_bits);
+    const H128 h = xxh3_128(key, len);
+    PosWalk pw(md, h.lo, h.hi);
+    for (uint32_t i = 0; i < k; i++) {
+        const uint32_t p = pw.pos();
+        words[p >> 6] |= 1ull << (p & 63);
+        pw.next(md);
+    }
+    return LSMB_OK;
+}
+
+int lsmb_may_contain(const uint64_t* words, uint32_t num_bits, uint32_t k, const uint8_t* key,
+                     uint64_t len) {
+    if (int rc = check_filter(num_bits, k)) return rc;
+    if (!k) return 1;
+    const Mod32 md = Mod32::make(num_bits);
+    const H128 h = xxh3_128(key, len);
+    PosWalk pw(md, h.lo, h.hi);
+    for (uint32_t i = 0; i < k; i++) {
+        const uint32_t p = pw.pos();
+        if (!((words[p >> 6] >> (p & 63)) & 1)) return 0;
+        pw.next(md);
+    }
+    return 1;
+}
+
+int lsmb_open(lsmb_ctx** out, int device) {
+    if (!out) return fail(LSMB_EINVAL, "null ctx pointer");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return fail(LSMB_ENODEV, "no HIP device visible (this engine runs its batched path on MI355X only)");
+    if (device < 0 && hipGetDevice(&device) != hipSuccess) device = 0;
+    if (device >= n) return fail(LSMB_ENODEV, "device %d out of range (%d visible)", device, n);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess)
+        return fail(LSMB_ENODEV, "hipGetDeviceProperties(%d) failed", device);
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(LSMB_ENODEV, "device %d is %s; kernels are built for gfx950 only", device, prop.gcnArchName);
+    lsmb_ctx* c = new lsmb_ctx;
+    c->dev = device;
+    c->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    DevGuard g(device);
+    if (hipStreamCreateWithFlags(&c->st, hipStreamDefault) != hipSuccess ||
+        hipEventCreateWithFlags(&c->desc_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreate(&c->tm.t0) != hipSuccess || hipEventCreate(&c->tm.t1) != hipSuccess ||
+        hipEventCreate(&c->tm.t2) != hipSuccess) {
+        delete c;
+        return fail(LSMB_ENODEV, "stream/event creation failed on device %d", device);
+    }
+    *out = c;
+    return LSMB_OK;
+}
+
+void lsmb_close(lsmb_ctx* c) {
+    if (!c) return;
+    {
+        DevGuard g(c->dev);
+        hipStreamSynchronize(c->st);
+        for (DevBuf* b : {&c->ws_bins, &c->ws_cursor, &c->keys, &c->offs, &c->words, &c->out,
+                          &c->filt_words, &c->filt_desc})
+            b->release();
+        hipEventDestroy(c->tm.t0);
+        hipEventDestroy(c->tm.t1);
+        hipEventDestroy(c->tm.t2);
+        hipEventDestroy(c->desc_done);
+        if (c->desc_pinned) hipHostFree(c->desc_pinned);
+        hipStreamDestroy(c->st);
+    }
+    delete c;
+}
+
+int lsmb_sync(lsmb_ctx* c) {
+    if (!c) return fail(LSMB_EINVAL, "null ctx");
+    DevGuard g(c->dev);
+    HIP_TRY(hipStreamSynchronize(c->st));
+    return LSMB_OK;
+}
+
+int lsmb_build_fixed_dev(lsmb_ctx* c, const void* d_keys, uint32_t key_len, uint64_t n,
+                         uint32_t num_bits, uint32_t k, void* d_words, void* stream) {
+    if (!c) return fail(LSMB_EINVAL, "null ctx");
+    if (int rc = check_filter(num_bits, k)) return rc;
+    if (n && (!d_keys || !d_words)) return fail(LSMB_EINVAL, "null device pointer");
+    if (n && key_len == 0) {
+        // every key is the empty key: one insert covers them all
+        KeyBatch kb{(const uint8_t*)d_keys, nullptr, 0, 1};
+        DevGuard g(c->dev);
+        return build_dev(c, kb, num_bits, k, (uint32_t*)d_words, pick_stream(c, stream));
+    }
+    DevGuard g(c->dev);
+    KeyBatch kb{(const uint8_t*)d_keys, nullptr, key_len, n};
+    return build_dev(c, kb, num_bits, k, (uint32_t*)d_words, pick_stream(c, stream));
+}
+
+int lsmb_build_var_dev(lsmb_ctx* c, const void* d_data, const void* d_offsets, uint64_t n,
+                       uint32_t num_bits, uint32_t k, void* d_words, void* stream) {
+    if (!c) return fail(LSMB_EINVAL, "null ctx");
+    if (int rc = check_filter(num_bits, k)) return rc;
+    if (n && (!d_offsets || !d_words)) return fail(LSMB_EINVAL, "null device pointer");
+    DevGuard g(c->dev);
+    KeyBatch kb{(const uint8_t*)d_data, (const uint64_t*)d_offsets, 0, n};
+    return build_dev(c, kb, num_bits, k, (uint32_t*)d_words, pick_stream(c, stream));
+}
+
+int lsmb_build_fixed(lsmb_ctx* c, const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t num_bits,
+                     uint32_t k, uint64_t* words) {
+    if (!c) return fail(LSMB_EINVAL, "null ctx");
+    if (int rc = check_filter(num_bits, k)) return rc;
+    if (n == 0 || k == 0) return LSMB_OK;
+    if (!keys && key_len) return fail(LSMB_EINVAL, "null keys");
+    if (!words) return fail(LSMB_EINVAL, "null words");
+    DevGuard g(c->dev);
+    const uint64_t nw = nwords64(num_bits);
+    HIP_TRY(c->words.ensure(nw * 8));
+    HIP_TRY(hipMemcpyAsync(c->words.p, words, nw * 8, hipMemcpyHostToDevice, c->st));
+    // H2D in chunks of <= 256 MiB of keys.
+    const uint64_t eff_len = key_len ? key_len : 1;
+    const uint64_t per = std::max<uint64_t>(1, (256ull << 20) / eff_len);
+    const uint64_t nn = key_len ? n : 1;  // all-empty keys: one insert
+    HIP_TRY(c->keys.ensure(std::min(per, nn) * eff_len + 16));
+    for (uint64_t f = 0; f < nn; f += per) {
+        const uint64_t m = std::min(per, nn - f);
+        if (key_len) HIP_TRY(hipMemcpyAsync(c->keys.p, keys + f * key_len, m * key_len, hipMemcpyHostToDevice, c->st));
+        KeyBatch kb{(const uint8_t*)c->keys.p, nullptr, key_len, m};
+        if (int rc = build_dev(c, kb, num_bits, k, (uint32_t*)c->words.p, c->st)) return rc;
+    }
+    HIP_TRY(hipMemcpyAsync(words, c->words.p, nw * 8, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    return LSMB_OK;
+}
+
+int lsmb_build_var(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, uint64_t n,
+                   uint32_t num_bits, uint32_t k, uint64_t* words) {
+    if (!c) return fail(LSMB_EINVAL, "null ctx");
+    if (int rc = check_filter(num_bits, k)) return rc;
+    if (n == 0 || k == 0) return LSMB_OK;
+    if (!offsets || !words) return fail(LSMB_EINVAL, "null pointer");
+    for (uint64_t i = 0; i < n; i++)
+        if (offsets[i + 1] < offsets[i]) return fail(LSMB_EINVAL, "offsets not non-decreasing at %llu", (unsigned long long)i);
+    DevGuard g(c->dev);
+    const uint64_t nw = nwords64(num_bits);
+    HIP_TRY(c->words.ensure(nw * 8));
+    HIP_TRY(hipMemcpyAsync(c->words.p, words, nw * 8, hipMemcpyHostToDevice, c->st));
+    const uint64_t budget = 256ull << 20;  // bytes of key data per chunk
+    uint64_t f = 0;
+    while (f < n) {
+        uint64_t e = f + 1;  // at least one key (a single key may exceed the budget)
+        while (e < n && offsets[e + 1] - offsets[f] <= budget && e - f < (32ull << 20)) e++;
+        const uint64_t bytes = offsets[e] - offsets[f];
+        HIP_TRY(c->keys.ensure(bytes + 16));
+        HIP_TRY(c->offs.ensure((e - f + 1) * 8));
+        c->offs_tmp.resize(e - f + 1);
+        for (uint64_t i = f; i <= e; i++) c->offs_tmp[i - f] = offsets[i] - offsets[f];
+        if (bytes) HIP_TRY(hipMemcpyAsync(c->keys.p, data + offsets[f], bytes, hipMemcpyHostToDevice, c->st));
+        HIP_TRY(hipMemcpyAsync(c->offs.p, c->offs_tmp.data(), (e - f + 1) * 8, hipMemcpyHostToDevice, c->st));
+        KeyBatch kb{(const uint8_t*)c->keys.p, (const uint64_t*)c->offs.p, 0, e - f};
+        if (int rc = build_dev(c, kb, num_bits, k, (uint32_t*)c->words.p, c->st)) return rc;
+        HIP_TRY(hipStreamSynchronize(c->st));  // offs_tmp is reused by the next chunk
+        f = e;
+    }
+    HIP_TRY(hipMemcpyAsync(words, c->words.p, nw * 8, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    return LSMB_OK;
+}
+
+static int probe_common(lsmb_ctx* c, const uint32_t* const* wptrs, const uint32_t* filt_bits,
+                        const uint32_t* filt_k, uint32_t nfilt, const KeyBatch& kb, uint8_t* d_out,
+                        hipStream_t st) {
+    if (nfilt == 0 || nfilt > 64) return fail(LSMB_EINVAL, "nfilt must be in [1, 64]");
+    c->hfilt.resize(nfilt);
+    for (uint32_t f = 0; f < nfilt; f++) {
+        if (int rc = check_filter(filt_bits[f], filt_k[f])) return rc;
+        ProbeFilter& p = c->hfilt[f];
+        memset(&p, 0, sizeof p);
+        p.words32 = wptrs[f];
+        p.md = filt_bits[f] ? Mod32::make(filt_bits[f]) : Mod32{1, ~0ull, 0};
+        p.num_bits = filt_bits[f];
+        p.k = filt_k[f];
+        p.out_bit = f;
+        p.group = f;
+    }
+    // Descriptors go to the device only when they change (a probe loop over the
+    // same level filters re-uses them); the upload waits for the last kernel
+    // that read the previous set, so no host sync sits between repeat probes.
+    HIP_TRY(c->filt_desc.ensure(sizeof(ProbeFilter) * 64));
+    const bool same = c->desc_uploaded.size() == nfilt &&
+                      memcmp(c->desc_uploaded.data(), c->hfilt.data(), sizeof(ProbeFilter) * nfilt) == 0;
+    if (!same) {
+        if (!c->desc_pinned) HIP_TRY(hipHostMalloc((void**)&c->desc_pinned, sizeof(ProbeFilter) * 64, 0));
+        HIP_TRY(hipEventSynchronize(c->desc_done));
+        memcpy(c->desc_pinned, c->hfilt.data(), sizeof(ProbeFilter) * nfilt);
+        HIP_TRY(hipMemcpyAsync(c->filt_desc.p, c->desc_pinned, sizeof(ProbeFilter) * nfilt,
+                               hipMemcpyHostToDevice, st));
+        c->desc_uploaded = c->hfilt;
+    }
+    HIP_TRY(launch_probe(kb, c->hfilt.data(), nfilt, (ProbeFilter*)c->filt_desc.p, d_out, c->num_cus, st));
+    HIP_TRY(hipEventRecord(c->desc_done, st));
+    return LSMB_OK;
+}
+
+int lsmb_probe_dev(lsmb_ctx* c, const void* const* d_filt_words, const uint32_t* filt_bits,
+                   const uint32_t* filt_k, uint32_t nfilt, const void* d_data, const void* d_offsets,
+                   uint32_t key_len, uint64_t n, void* d_out, void* stream) {
+    if (!c) return fail(LSMB_EINVAL, "null ctx");
+    if (!d_filt_words || !filt_bits || !filt_k) return fail(LSMB_EINVAL, "null filter arrays");
+    if (n && !d_out) return fail(LSMB_EINVAL, "null output");
+    DevGuard g(c->dev);
+    KeyBatch kb{(const uint8_t*)d_data, (const uint64_t*)d_offsets, key_len, n};
+    return probe_common(c, (const uint32_t* const*)d_filt_words, filt_bits, filt_k, nfilt, kb,
+                        (uint8_t*)d_out, pick_stream(c, stream));
+}
+
+int lsmb_probe(lsmb_ctx* c, const uint64_t* const* filt_words, const uint32_t* filt_bits,
+               const uint32_t* filt_k, uint32_t nfilt, const uint8_t* data, const uint64_t* offsets,
+               uint32_t key_len, uint64_t n, uint8_t* out) {
+    if (!c) return fail(LSMB_EINVAL, "null ctx");
+    if (!filt_words || !filt_bits || !filt_k) return fail(LSMB_EINVAL, "null filter arrays");
+    if (nfilt == 0 || nfilt > 64) return fail(LSMB_EINVAL, "nfilt must be in [1, 64]");
+    if (n == 0) return LSMB_OK;
+    if (!out) return fail(LSMB_EINVAL, "null output");
+    DevGuard g(c->dev);
+    // filters -> one device arena
+    uint64_t tot = 0;
+    std::vector<uint64_t> at(nfilt);
+    for (uint32_t f = 0; f < nfilt; f++) {
+        at[f] = tot;
+        tot += (nwords64(filt_bits[f]) + 1) & ~1ull;  // keep 16-B alignment
+    }
+    HIP_TRY(c->filt_words.ensure(std::max<uint64_t>(tot, 2) * 8));
+    std::vector<const uint32_t*> dptr(nfilt);
+    for (uint32_t f = 0; f < nfilt; f++) {
+        uint64_t* d = (uint64_t*)c->filt_words.p + at[f];
+        if (nwords64(filt_bits[f]))
+            HIP_TRY(hipMemcpyAsync(d, filt_words[f], nwords64(filt_bits[f]) * 8, hipMemcpyHostToDevice, c->st));
+        dptr[f] = (const uint32_t*)d;
+    }
+    const uint32_t stride = (nfilt + 7) / 8;
+    HIP_TRY(c->out.ensure(n * stride));
+    uint64_t kbytes;
+    if (offsets) {
+        for (uint64_t i = 0; i < n; i++)
+            if (offsets[i + 1] < offsets[i]) return fail(LSMB_EINVAL, "offsets not non-decreasing");
+        kbytes = offsets[n] - offsets[0];
+        c->offs_tmp.resize(n + 1);
+        for (uint64_t i = 0; i <= n; i++) c->offs_tmp[i] = offsets[i] - offsets[0];
+        HIP_TRY(c->offs.ensure((n + 1) * 8));
+        HIP_TRY(hipMemcpyAsync(c->offs.p, c->offs_tmp.data(), (n + 1) * 8, hipMemcpyHostToDevice, c->st));
+        HIP_TRY(c->keys.ensure(kbytes + 16));
+        if (kbytes) HIP_TRY(hipMemcpyAsync(c->keys.p, data + offsets[0], kbytes, hipMemcpyHostToDevice, c->st));
+    } else {
+        kbytes = (uint64_t)key_len * n;
+        HIP_TRY(c->keys.ensure(kbytes + 16));
+        if (kbytes) HIP_TRY(hipMemcpyAsync(c->keys.p, data, kbytes, hipMemcpyHostToDevice, c->st));
+    }
+    KeyBatch kb{(const uint8_t*)c->keys.p, offsets ? (const uint64_t*)c->offs.p : nullptr, key_len, n};
+    if (int rc = probe_common(c, dptr.data(), filt_bits, filt_k, nfilt, kb, (uint8_t*)c->out.p, c->st)) return rc;
+    HIP_TRY(hipMemcpyAsync(out, c->out.p, n * stride, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    return LSMB_OK;
+}
+
+int lsmb_or_reduce_dev(lsmb_ctx* c, void* dst, const void* src, uint64_t nwords, uint32_t nsrc,
+                       uint64_t stride_words, void* stream) {
+    if (!c) return fail(LSMB_EINVAL, "null ctx");
+    if (nwords == 0 || nsrc == 0) return LSMB_OK;
+    DevGuard g(c->dev);
+    HIP_TRY(launch_or_reduce((uint32_t*)dst, (const uint32_t*)src, 2 * nwords, nsrc, 2 * stride_words,
+                             pick_stream(c, stream)));
+    return LSMB_OK;
+}
+
+int lsmb_gen_key16_dev(lsmb_ctx* c, uint64_t seed, uint64_t first, uint64_t n, void* d_keys, void* stream) {
+    if (!c) return fail(LSMB_EINVAL, "null ctx");
+    if (n == 0) return LSMB_OK;
+    if (reinterpret_cast<uintptr_t>(d_keys) & 15) return fail(LSMB_EINVAL, "d_keys must be 16-byte aligned");
+    DevGuard g(c->dev);
+    HIP_TRY(launch_gen_key16(seed, first, n, (uint8_t*)d_keys, pick_stream(c, stream)));
+    return LSMB_OK;
+}
+
+const char* lsmb_build_strategy(uint32_t num_bits, uint64_t n) {
+    return strategy_name(pick_build_strategy(num_bits, 7, n));
+}
+
+int lsmb_last_build_ms(lsmb_ctx* c, float* out3) {
+    if (!c || !out3) return fail(LSMB_EINVAL, "null argument");
+    if (!c->tm.valid) return fail(LSMB_EINVAL, "no timed build on this context");
+    DevGuard g(c->dev);
+    HIP_TRY(hipEventElapsedTime(&out3[0], c->tm.t0, c->tm.t2));
+    HIP_TRY(hipEventElapsedTime(&out3[1], c->tm.t0, c->tm.t1));
+    HIP_TRY(hipEventElapsedTime(&out3[2], c->tm.t1, c->tm.t2));
+    return LSMB_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,46 @@
+// keysrc.hpp — how the kernels read one key and hash it (device side, internal).
+#pragma once
+
+#include "bloom_math.hpp"
+
+namespace lsmb {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// 16-byte streaming load that bypasses cache allocation (read-once data).
+__device__ __forceinline__ uint4 ld_stream16(const uint4* p) {
+    u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+namespace ks {
+
+// 16-byte keys on a 16-byte-aligned base: one dwordx4 load per key, streamed
+// past the caches (each key is read exactly once).
+struct Fixed16 {
+    const uint4* k;
+    __device__ __forceinline__ H128 hash(uint64_t i) const {
+        uint4 v = ld_stream16(k + i);
+        return xxh3_16(((uint64_t)v.y << 32) | v.x, ((uint64_t)v.w << 32) | v.z);
+    }
+};
+
+// Any fixed key length, any alignment.
+struct FixedN {
+    const uint8_t* d;
+    uint32_t len;
+    __device__ __forceinline__ H128 hash(uint64_t i) const { return xxh3_128(d + i * len, len); }
+};
+
+// Packed variable-length keys: key i = d[o[i] .. o[i+1]).
+struct VarLen {
+    const uint8_t* d;
+    const uint64_t* o;
+    __device__ __forceinline__ H128 hash(uint64_t i) const {
+        uint64_t a = o[i], b = o[i + 1];
+        return xxh3_128(d + a, b - a);
+    }
+};
+
+}  // namespace ks
+}  // namespace lsmb

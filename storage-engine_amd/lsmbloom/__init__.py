@@ -1,0 +1,352 @@
+"""lsmbloom — Python binding of the MI355X Bloom engine's C ABI (include/lsmbloom.h).
+
+Mirrors the reference's Rust surface `crate::bloom` (G1DO/Storage-Engine
+src/bloom/mod.rs, src/bloom/builder.rs) so tests read like the reference's own:
+
+    bf = BloomFilter.new(100, 0.01)      # BloomFilter::new            mod.rs:38-67
+    bf.insert(b"hello")                  # BloomFilter::insert         mod.rs:70-78
+    bf.may_contain(b"hello")             # BloomFilter::may_contain    mod.rs:82-94
+    bf.serialize() / BloomFilter.deserialize(b)                      # mod.rs:102-168
+    b = BloomFilterBuilder.new(n, fpr); b.add_key(k); bf = b.build()  # builder.rs:14-28
+
+Batched work (BloomFilterBuilder.build, probe_batch) runs on the GPU through
+the C ABI; it raises if the HIP library or a gfx950 device is missing — there
+is no CPU fallback.  Device-resident entry points take torch tensors.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "liblsmbloom.so")
+
+LSMB_OK = 0
+LSMB_EINVAL = -1
+LSMB_ENODEV = -2
+LSMB_EHIP = -3
+LSMB_ECORRUPT = -4
+LSMB_ENOMEM = -5
+
+u8p = ctypes.POINTER(ctypes.c_uint8)
+u32p = ctypes.POINTER(ctypes.c_uint32)
+u64p = ctypes.POINTER(ctypes.c_uint64)
+vp = ctypes.c_void_p
+
+# name -> (restype, argtypes); the exact export list of include/lsmbloom.h
+SIGNATURES = {
+    "lsmb_abi_version": (ctypes.c_int, []),
+    "lsmb_last_error": (ctypes.c_char_p, []),
+    "lsmb_params": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_double, u32p, u32p]),
+    "lsmb_num_words": (ctypes.c_uint64, [ctypes.c_uint32]),
+    "lsmb_serialized_size": (ctypes.c_uint64, [ctypes.c_uint32]),
+    "lsmb_serialize": (ctypes.c_int, [u64p, ctypes.c_uint32, ctypes.c_uint32, u8p, ctypes.c_uint64]),
+    "lsmb_deserialize_header": (ctypes.c_int, [u8p, ctypes.c_uint64, u32p, u32p, u32p]),
+    "lsmb_deserialize": (ctypes.c_int, [u8p, ctypes.c_uint64, u64p, ctypes.c_uint64]),
+    "lsmb_insert": (ctypes.c_int, [u64p, ctypes.c_uint32, ctypes.c_uint32, u8p, ctypes.c_uint64]),
+    "lsmb_may_contain": (ctypes.c_int, [u64p, ctypes.c_uint32, ctypes.c_uint32, u8p, ctypes.c_uint64]),
+    "lsmb_positions": (ctypes.c_int, [u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, u32p]),
+    "lsmb_open": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_int]),
+    "lsmb_close": (None, [vp]),
+    "lsmb_sync": (ctypes.c_int, [vp]),
+    "lsmb_build_fixed": (ctypes.c_int, [vp, u8p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
+                                        ctypes.c_uint32, u64p]),
+    "lsmb_build_var": (ctypes.c_int, [vp, u8p, u64p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, u64p]),
+    "lsmb_probe": (ctypes.c_int, [vp, ctypes.POINTER(u64p), u32p, u32p, ctypes.c_uint32, u8p, u64p,
+                                  ctypes.c_uint32, ctypes.c_uint64, u8p]),
+    "lsmb_build_fixed_dev": (ctypes.c_int, [vp, vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
+                                            ctypes.c_uint32, vp, vp]),
+    "lsmb_build_var_dev": (ctypes.c_int, [vp, vp, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                          vp, vp]),
+    "lsmb_probe_dev": (ctypes.c_int, [vp, ctypes.POINTER(vp), u32p, u32p, ctypes.c_uint32, vp, vp,
+                                      ctypes.c_uint32, ctypes.c_uint64, vp, vp]),
+    "lsmb_or_reduce_dev": (ctypes.c_int, [vp, vp, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, vp]),
+    "lsmb_gen_key16_dev": (ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, vp, vp]),
+    "lsmb_build_strategy": (ctypes.c_char_p, [ctypes.c_uint32, ctypes.c_uint64]),
+    "lsmb_last_build_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_float)]),
+}
+
+_lib = None
+
+
+class LsmbError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("lsmb error %d: %s" % (code, msg))
+        self.code = code
+
+
+class Corruption(LsmbError):
+    """Error::Corruption(String) of the reference (src/error.rs:12)."""
+
+
+def lib():
+    """Loads liblsmbloom.so; raises if the HIP library was not built (no fallback)."""
+    global _lib
+    if _lib is None:
+        # Load torch's HIP runtime FIRST when torch is present: liblsmbloom.so
+        # needs libamdhip64.so.7, and torch ships its own copy under the same
+        # SONAME, so the loader then binds us to torch's runtime.  One runtime
+        # per process means torch tensors, torch streams and RCCL share device
+        # state with our kernels (loading ours first would start a second
+        # runtime and break torch's CUDA init).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("liblsmbloom.so not built (%s); run `make -C storage-engine_amd`" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc < 0:
+        msg = lib().lsmb_last_error().decode(errors="replace")
+        if rc == LSMB_ECORRUPT:
+            raise Corruption(rc, msg)
+        if rc == LSMB_EINVAL:
+            raise ValueError(msg)
+        raise LsmbError(rc, msg)
+    return rc
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+def _key(b):
+    b = bytes(b)
+    a = np.frombuffer(b + b"\0", dtype=np.uint8)
+    return a, len(b)
+
+
+def params(expected_items, false_positive_rate):
+    """BloomFilter::new sizing -> (num_bits, num_hashes); ValueError where the reference panics."""
+    nb, k = ctypes.c_uint32(), ctypes.c_uint32()
+    _check(lib().lsmb_params(int(expected_items), float(false_positive_rate), ctypes.byref(nb), ctypes.byref(k)))
+    return nb.value, k.value
+
+
+def num_words(num_bits):
+    return int(lib().lsmb_num_words(num_bits))
+
+
+def positions(key, num_bits, k):
+    a, n = _key(key)
+    out = np.zeros(max(k, 1), dtype=np.uint32)
+    _check(lib().lsmb_positions(_p(a, u8p), n, num_bits, k, _p(out, u32p)))
+    return [int(x) for x in out[:k]]
+
+
+# ------------------------------------------------------------------ GPU context
+class Context:
+    """One GPU: stream + scratch arenas (lsmb_ctx).  Raises if no gfx950 device."""
+
+    def __init__(self, device=-1):
+        h = vp()
+        _check(lib().lsmb_open(ctypes.byref(h), int(device)))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            lib().lsmb_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self):
+        _check(lib().lsmb_sync(self.h))
+
+    # host-memory entry points -------------------------------------------------
+    def build_fixed(self, keys, key_len, num_bits, k, words=None):
+        keys = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1)
+        n = keys.size // key_len if key_len else 0
+        if words is None:
+            words = np.zeros(num_words(num_bits), dtype=np.uint64)
+        if keys.size == 0:
+            keys = np.zeros(1, np.uint8)
+        _check(lib().lsmb_build_fixed(self.h, _p(keys, u8p), key_len, n, num_bits, k, _p(words, u64p)))
+        return words
+
+    def build_var(self, data, offsets, num_bits, k, words=None):
+        data = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        if words is None:
+            words = np.zeros(num_words(num_bits), dtype=np.uint64)
+        if data.size == 0:
+            data = np.zeros(1, np.uint8)
+        _check(lib().lsmb_build_var(self.h, _p(data, u8p), _p(offsets, u64p), offsets.size - 1, num_bits, k,
+                                    _p(words, u64p)))
+        return words
+
+    def probe(self, filters, data, offsets=None, key_len=0):
+        """filters: [(words uint64 array, num_bits, k)] -> uint8 [n, ceil(F/8)] mask."""
+        F = len(filters)
+        ws = [np.ascontiguousarray(f[0], dtype=np.uint64) for f in filters]
+        arr = (u64p * F)(*[_p(w, u64p) for w in ws])
+        nb = np.array([f[1] for f in filters], dtype=np.uint32)
+        kk = np.array([f[2] for f in filters], dtype=np.uint32)
+        data = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+        if offsets is not None:
+            offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+            n = offsets.size - 1
+            op = _p(offsets, u64p)
+        else:
+            n = data.size // key_len if key_len else 0
+            op = None
+        out = np.zeros((n, (F + 7) // 8), dtype=np.uint8)
+        if data.size == 0:
+            data = np.zeros(1, np.uint8)
+        _check(lib().lsmb_probe(self.h, arr, _p(nb, u32p), _p(kk, u32p), F, _p(data, u8p), op, key_len, n,
+                                _p(out, u8p)))
+        return out
+
+    # device-resident entry points (torch tensors) ------------------------------
+    @staticmethod
+    def _stream(stream):
+        if stream is None:
+            import torch
+            return vp(torch.cuda.current_stream().cuda_stream)
+        return vp(stream)
+
+    def build_fixed_dev(self, keys, key_len, n, num_bits, k, words, stream=None):
+        _check(lib().lsmb_build_fixed_dev(self.h, vp(keys.data_ptr()), key_len, n, num_bits, k,
+                                          vp(words.data_ptr()), self._stream(stream)))
+
+    def build_var_dev(self, data, offsets, n, num_bits, k, words, stream=None):
+        _check(lib().lsmb_build_var_dev(self.h, vp(data.data_ptr()), vp(offsets.data_ptr()), n, num_bits, k,
+                                        vp(words.data_ptr()), self._stream(stream)))
+
+    def probe_dev(self, filters, data, n, out, offsets=None, key_len=0, stream=None):
+        """filters: [(words tensor on device, num_bits, k)]."""
+        F = len(filters)
+        arr = (vp * F)(*[vp(f[0].data_ptr()) for f in filters])
+        nb = np.array([f[1] for f in filters], dtype=np.uint32)
+        kk = np.array([f[2] for f in filters], dtype=np.uint32)
+        _check(lib().lsmb_probe_dev(self.h, arr, _p(nb, u32p), _p(kk, u32p), F, vp(data.data_ptr()),
+                                    vp(offsets.data_ptr()) if offsets is not None else None, key_len, n,
+                                    vp(out.data_ptr()), self._stream(stream)))
+
+    def or_reduce_dev(self, dst, src, nwords, nsrc, stride_words, stream=None):
+        _check(lib().lsmb_or_reduce_dev(self.h, vp(dst.data_ptr()), vp(src.data_ptr()), nwords, nsrc,
+                                        stride_words, self._stream(stream)))
+
+    def gen_key16_dev(self, seed, first, n, out, stream=None):
+        _check(lib().lsmb_gen_key16_dev(self.h, seed, first, n, vp(out.data_ptr()), self._stream(stream)))
+
+    def last_build_ms(self):
+        a = (ctypes.c_float * 3)()
+        _check(lib().lsmb_last_build_ms(self.h, a))
+        return tuple(a)
+
+
+def build_strategy(num_bits, n):
+    return lib().lsmb_build_strategy(num_bits, n).decode()
+
+
+_default_ctx = None
+
+
+def default_context():
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(-1)
+    return _default_ctx
+
+
+# ------------------------------------------------------------------ reference surface
+class BloomFilter:
+    """Mirror of `pub struct BloomFilter` (src/bloom/mod.rs:23-27): words + num_hashes + num_bits."""
+
+    __slots__ = ("bits", "_k", "_nb")
+
+    def __init__(self, bits, num_hashes, num_bits):
+        self.bits = bits
+        self._k = num_hashes
+        self._nb = num_bits
+
+    @classmethod
+    def new(cls, expected_items, false_positive_rate):
+        nb, k = params(expected_items, false_positive_rate)
+        return cls(np.zeros(num_words(nb), dtype=np.uint64), k, nb)
+
+    def insert(self, key):
+        a, n = _key(key)
+        _check(lib().lsmb_insert(_p(self.bits, u64p), self._nb, self._k, _p(a, u8p), n))
+
+    def may_contain(self, key):
+        a, n = _key(key)
+        return bool(_check(lib().lsmb_may_contain(_p(self.bits, u64p), self._nb, self._k, _p(a, u8p), n)))
+
+    def serialize(self):
+        size = int(lib().lsmb_serialized_size(self._nb))
+        out = np.zeros(size, dtype=np.uint8)
+        _check(lib().lsmb_serialize(_p(self.bits, u64p), self._nb, self._k, _p(out, u8p), size))
+        return out.tobytes()
+
+    @classmethod
+    def deserialize(cls, data):
+        a, n = _key(data)
+        k, nb, nw = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        _check(lib().lsmb_deserialize_header(_p(a, u8p), n, ctypes.byref(k), ctypes.byref(nb), ctypes.byref(nw)))
+        words = np.zeros(nw.value, dtype=np.uint64)
+        _check(lib().lsmb_deserialize(_p(a, u8p), n, _p(words, u64p), nw.value))
+        return cls(words, k.value, nb.value)
+
+    def num_hashes(self):
+        return self._k
+
+    def num_bits(self):
+        return self._nb
+
+    # additive batched API (the reference has no multi-get)
+    @staticmethod
+    def may_contain_batch(filters, keys, ctx=None):
+        """keys: list of bytes.  Returns uint8 [len(keys), ceil(F/8)] mask (GPU)."""
+        ctx = ctx or default_context()
+        offs = np.zeros(len(keys) + 1, dtype=np.uint64)
+        if keys:
+            offs[1:] = np.cumsum([len(k) for k in keys])
+        data = np.frombuffer(b"".join(bytes(k) for k in keys), dtype=np.uint8)
+        return ctx.probe([(f.bits, f._nb, f._k) for f in filters], data, offs)
+
+
+class BloomFilterBuilder:
+    """Mirror of `BloomFilterBuilder` (src/bloom/builder.rs:8-28).
+
+    The reference inserts on the fly (builder.rs:21-23); this one buffers the
+    run's keys in a packed arena and builds the whole filter in one GPU batch
+    at `build()`.  The bits are identical.
+    """
+
+    def __init__(self, filt, ctx=None):
+        self._filter = filt
+        self._data = bytearray()
+        self._offs = [0]
+        self._ctx = ctx
+
+    @classmethod
+    def new(cls, estimated_keys, false_positive_rate, ctx=None):
+        return cls(BloomFilter.new(estimated_keys, false_positive_rate), ctx)
+
+    def add_key(self, key):
+        self._data += bytes(key)
+        self._offs.append(len(self._data))
+
+    def build(self):
+        f = self._filter
+        if len(self._offs) > 1:
+            ctx = self._ctx or default_context()
+            offs = np.array(self._offs, dtype=np.uint64)
+            data = np.frombuffer(bytes(self._data), dtype=np.uint8)
+            ctx.build_var(data, offs, f._nb, f._k, f.bits)
+        return f

@@ -1,0 +1,63 @@
+"""Multi-GPU: merge per-rank partial filters with a bitwise-OR allreduce.
+
+A sharded build (each rank hashes its contiguous slice of one run's keys into
+a full-size partial filter) is exact because OR is associative, commutative and
+idempotent: OR of the partials == the single-device filter, bit for bit.
+
+RCCL has no bitwise-OR reduction (rccl.h ncclRedOp_t: sum/prod/max/min/avg),
+so the allreduce is composed from op-free collectives:
+  1. reduce-scatter: all_to_all_single sends word-slice j of my partial to rank j;
+  2. each rank ORs the G slices it received (native kernel, lsmb_or_reduce_dev);
+  3. all_gather_into_tensor returns the merged slices to every rank.
+Per-GPU traffic is 2 (G-1)/G x filter bytes; over xGMI's point-to-point links
+the all_to_all phase uses every peer link at once.  The end-to-end variant
+(`or_reduce_scatter_`) stops after step 2: each rank then copies its own slice
+to host memory, which parallelises the D2H over the ranks' PCIe links.
+"""
+import torch
+import torch.distributed as dist
+
+
+def _slices(n, world):
+    per = (n + world - 1) // world
+    per = (per + 1) & ~1  # even: 16-B aligned slices of int64 words
+    return per
+
+
+def or_reduce_scatter_(words, group=None, ctx=None):
+    """Returns (slice_tensor, start_word): this rank's merged slice of the filter."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    n = words.numel()
+    per = _slices(n, world)
+    if per * world != n:
+        buf = torch.zeros(per * world, dtype=words.dtype, device=words.device)
+        buf[:n].copy_(words)
+    else:
+        buf = words
+    recv = torch.empty_like(buf)
+    dist.all_to_all_single(recv, buf, group=group)
+    mine = torch.empty(per, dtype=words.dtype, device=words.device)
+    if words.is_cuda and ctx is not None:
+        mine.zero_()
+        ctx.or_reduce_dev(mine, recv, per, world, per)
+    else:
+        r = recv.view(world, per)
+        mine.copy_(r[0])
+        for j in range(1, world):
+            mine.bitwise_or_(r[j])
+    return mine, rank * per
+
+
+def or_allreduce_(words, group=None, ctx=None):
+    """In-place bitwise-OR allreduce of an int64 word tensor across the group."""
+    world = dist.get_world_size(group)
+    if world == 1:
+        return words
+    n = words.numel()
+    mine, _ = or_reduce_scatter_(words, group, ctx)
+    per = mine.numel()
+    out = torch.empty(per * world, dtype=words.dtype, device=words.device)
+    dist.all_gather_into_tensor(out, mine, group=group)
+    words.copy_(out[:n])
+    return words

@@ -99,7 +99,7 @@ class Oracle:
 
     def build_fixed_mt(self, keys, key_len, num_bits, k, threads, words=None):
         keys = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1)
-        n = keys.size // key_len
+        n = keys.size // key_len if key_len else 0
         if words is None:
             words = np.zeros(self.nwords(num_bits), dtype=np.uint64)
         rc = self.lib.oracle_bloom_build_fixed_mt(_p(keys, u8p), key_len, n, num_bits, k,

@@ -1,0 +1,299 @@
+"""GPU parity: the HIP build/probe path (through the C ABI) vs the CPU oracle.
+
+Bit-exact for every word of every filter and every probe answer.  Small cases
+compare against the committed golden fixtures; larger ones against the oracle
+(oracle/liboracle.so, the checker) on the same seeded inputs, up to the full
+BASELINE C2 size (100 M keys) where the multi-threaded oracle finishes in seconds.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import keygen
+import lsmbloom
+from lsmbloom import BloomFilter, BloomFilterBuilder
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+KATS = json.load(open(os.path.join(GOLD, "bloom_kats.json")))
+C1 = json.load(open(os.path.join(GOLD, "c1_fixture.json")))
+VAR = json.load(open(os.path.join(GOLD, "varlen_fixture.json")))
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = lsmbloom.Context(0)
+    yield c
+    c.close()
+
+
+def sha(b):
+    return hashlib.sha256(bytes(b)).hexdigest()
+
+
+def ser(words, nb, k):
+    f = BloomFilter(words, k, nb)
+    return f.serialize()
+
+
+# ---------------------------------------------------------------- golden fixtures
+def test_c1_fixture_gpu(ctx):
+    keys = keygen.key16(0x5EED0001, 0, C1["n"])
+    nb, k = lsmbloom.params(C1["n"], 0.01)
+    assert lsmbloom.build_strategy(nb, C1["n"]) == "lds"
+    w = ctx.build_fixed(keys, 16, nb, k)
+    assert sha(ser(w, nb, k)) == C1["serialized_sha256"]
+    nm = keygen.key16(0x5EED0002, 0, C1["n"])
+    m = ctx.probe([(w, nb, k)], nm, key_len=16)
+    assert int(m.sum()) == C1["nonmember_false_positives"]
+    assert sha(m.reshape(-1)) == C1["nonmember_probe_sha256"]
+    assert ctx.probe([(w, nb, k)], keys, key_len=16).all()  # no false negatives
+
+
+def test_reference_scenarios_gpu_builder(ctx):
+    for sc in KATS["scenarios"]:
+        b = BloomFilterBuilder.new(sc["n"], sc["fpr"], ctx=ctx)
+        for key in sc["inserts"]:
+            b.add_key(bytes.fromhex(key))
+        bf = b.build()
+        assert sha(bf.serialize()) == sc["serialized_sha256"], sc["name"]
+        probes = [bytes.fromhex(p[0]) for p in sc["probes"]]
+        m = BloomFilter.may_contain_batch([bf], probes, ctx=ctx)
+        assert [bool(x) for x in m[:, 0]] == [p[1] for p in sc["probes"]], sc["name"]
+
+
+def test_reference_fpr_counts_gpu(ctx):
+    from test_oracle_golden import _fmt_keys
+    for c in KATS["counts"]:
+        ins, probes = _fmt_keys(c)
+        nb, k = lsmbloom.params(c["n"], c["fpr"])
+        d, o = keygen.pack(ins)
+        w = ctx.build_var(d, o, nb, k)
+        assert sha(ser(w, nb, k)) == c["serialized_sha256"], c["name"]
+        pd, po = keygen.pack(probes)
+        m = ctx.probe([(w, nb, k)], pd, po)
+        if "false_positives" in c:
+            assert int(m.sum()) == c["false_positives"], c["name"]
+
+
+def test_varlen_fixture_gpu(ctx):
+    data, offs = keygen.varlen(VAR["n"])
+    nb, k = lsmbloom.params(VAR["n"], 0.01)
+    w = ctx.build_var(data, offs, nb, k)
+    assert sha(ser(w, nb, k)) == VAR["serialized_sha256"]
+    nm = keygen.key16(0x5EED0002, 0, VAR["n"])
+    assert int(ctx.probe([(w, nb, k)], nm, key_len=16).sum()) == VAR["nonmember_false_positives"]
+
+
+# ---------------------------------------------------------------- oracle parity
+def _cmp(a, b):
+    assert a.shape == b.shape
+    bad = np.nonzero(a != b)[0]
+    assert bad.size == 0, "first mismatching words: %s" % bad[:8]
+
+
+@pytest.mark.parametrize("n,fpr", [(1, 0.01), (1000, 0.01), (70_000, 0.001), (300_000, 0.01),
+                                   (2_000_001, 0.01), (5_000_000, 0.05)])
+def test_build_fixed16_vs_oracle(ctx, oracle, n, fpr):
+    keys = keygen.key16(0x5EED0001, 0, n)
+    nb, k = lsmbloom.params(n, fpr)
+    _cmp(ctx.build_fixed(keys, 16, nb, k), oracle.build_fixed(keys, 16, nb, k))
+
+
+def test_build_partition_huge_filter(ctx, oracle):
+    # the C5 filter: new(1e9, 0.01) saturates to 2^32-1 bits (mod.rs:49), 512 MiB
+    n = 3_000_000
+    nb, k = lsmbloom.params(10**9, 0.01)
+    assert nb == 2**32 - 1
+    keys = keygen.key16(0x5EED0001, 0, n)
+    assert lsmbloom.build_strategy(nb, n) == "partition"
+    _cmp(ctx.build_fixed(keys, 16, nb, k), oracle.build_fixed_mt(keys, 16, nb, k, 16))
+
+
+def test_build_few_keys_huge_filter_atomic(ctx, oracle):
+    nb, k = lsmbloom.params(10**8, 0.01)
+    keys = keygen.key16(0x1234, 0, 1000)
+    assert lsmbloom.build_strategy(nb, 1000) == "atomic"
+    _cmp(ctx.build_fixed(keys, 16, nb, k), oracle.build_fixed(keys, 16, nb, k))
+
+
+def test_build_duplicate_heavy_overflow(ctx, oracle):
+    # 2M copies of one key + 1M distinct: a few slices receive far more than
+    # their expected share, exercising the run-overflow path.
+    n = 3_000_000
+    keys = keygen.key16(0xD00D, 0, n)
+    keys[: 2_000_000] = keys[0]
+    nb, k = lsmbloom.params(n, 0.01)
+    _cmp(ctx.build_fixed(keys, 16, nb, k), oracle.build_fixed_mt(keys, 16, nb, k, 16))
+
+
+def test_build_or_accumulates(ctx, oracle):
+    n = 500_000
+    nb, k = lsmbloom.params(2 * n, 0.01)
+    a = keygen.key16(1, 0, n)
+    b = keygen.key16(2, 0, n)
+    w = ctx.build_fixed(a, 16, nb, k)
+    w = ctx.build_fixed(b, 16, nb, k, words=w)
+    ref = oracle.build_fixed(b, 16, nb, k, words=oracle.build_fixed(a, 16, nb, k))
+    _cmp(w, ref)
+
+
+@pytest.mark.parametrize("key_len", [1, 3, 4, 7, 8, 9, 12, 15, 16, 17, 31, 64, 100, 128, 129, 200,
+                                     240, 241, 256, 300, 1024, 1025, 4000])
+def test_build_fixed_len_vs_oracle(ctx, oracle, key_len):
+    n = 20_000 if key_len <= 300 else 2000
+    data = keygen.stream_bytes(0xABC + key_len, n * key_len)
+    for fpr in (0.01,):
+        nb, k = lsmbloom.params(n, fpr)
+        _cmp(ctx.build_fixed(data, key_len, nb, k), oracle.build_fixed(data, key_len, nb, k))
+    nb, k = lsmbloom.params(50 * n, 0.01)  # partition strategy for bigger filters
+    _cmp(ctx.build_fixed(data, key_len, nb, k), oracle.build_fixed(data, key_len, nb, k))
+
+
+def test_build_var_every_length_class(ctx, oracle):
+    rng = np.random.default_rng(3)
+    lens = list(range(0, 301)) * 20 + [511, 1023, 1024, 1025, 2048, 4097, 10000]
+    rng.shuffle(lens)
+    blob = keygen.stream_bytes(0x77, int(sum(lens)))
+    offs = np.zeros(len(lens) + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    for n_exp in (len(lens), 40 * len(lens)):
+        nb, k = lsmbloom.params(n_exp, 0.01)
+        _cmp(ctx.build_var(blob, offs, nb, k), oracle.build_var(blob, offs, nb, k))
+
+
+def test_build_var_c4_shape(ctx, oracle):
+    n = 1_000_000
+    data, offs = keygen.varlen(n)
+    nb, k = lsmbloom.params(n, 0.01)
+    _cmp(ctx.build_var(data, offs, nb, k), oracle.build_var(data, offs, nb, k))
+
+
+@pytest.mark.parametrize("k", [1, 2, 7, 8, 9, 16, 17, 32, 33, 40])
+def test_build_any_k(ctx, oracle, k):
+    n = 200_000
+    keys = keygen.key16(0xBEE + k, 0, n)
+    for nb in (5000, 4_000_003):
+        _cmp(ctx.build_fixed(keys, 16, nb, k), oracle.build_fixed(keys, 16, nb, k))
+
+
+# ---------------------------------------------------------------- probe
+def _c3_filters(oracle, nfilt=8, members=1000):
+    nb, k = lsmbloom.params(1000, 0.01)  # SSTableBuilder::new sizing
+    fl, mem = [], []
+    for f in range(nfilt):
+        keys = keygen.key16(0xF000 + f, 0, members)
+        fl.append((oracle.build_fixed(keys, 16, nb, k), nb, k))
+        mem.append(keys)
+    return fl, np.concatenate(mem)
+
+
+@pytest.mark.parametrize("nfilt", [1, 3, 8, 9, 16, 17, 32])
+def test_probe_sliced_vs_oracle(ctx, oracle, nfilt):
+    fl, mem = _c3_filters(oracle, nfilt)
+    q = 200_000
+    rng = np.random.default_rng(nfilt)
+    fresh = keygen.key16(0xAAAA, 0, q // 2)
+    hits = mem[rng.integers(0, mem.shape[0], q - q // 2)]
+    keys = np.concatenate([fresh, hits])
+    got = ctx.probe(fl, keys, key_len=16)
+    ref = oracle.probe(fl, keys, key_len=16)
+    assert np.array_equal(got, ref)
+
+
+def test_probe_generic_mixed_filters(ctx, oracle):
+    fl = []
+    for i, (n, fpr) in enumerate([(1000, 0.01), (50_000, 0.001), (300_000, 0.05), (10, 0.5), (2_000_000, 0.01)]):
+        nb, k = lsmbloom.params(n, fpr)
+        keys = keygen.key16(0x5000 + i, 0, n)
+        fl.append((oracle.build_fixed(keys, 16, nb, k), nb, k))
+    fl.append((np.zeros(0, np.uint64), 0, 0))  # num_bits = 0, k = 0: always true
+    q = 100_000
+    keys = np.concatenate([keygen.key16(0x5001, 0, q // 2), keygen.key16(0x9999, 0, q // 2)])
+    assert np.array_equal(ctx.probe(fl, keys, key_len=16), oracle.probe(fl, keys, key_len=16))
+    data, offs = keygen.varlen(30_000)
+    assert np.array_equal(ctx.probe(fl, data, offs), oracle.probe(fl, data, offs))
+
+
+def test_probe_many_filters_64(ctx, oracle):
+    fl = []
+    for f in range(64):
+        nb, k = lsmbloom.params(200 + 10 * f, 0.01)
+        fl.append((oracle.build_fixed(keygen.key16(0x6000 + f, 0, 200), 16, nb, k), nb, k))
+    keys = np.concatenate([keygen.key16(0x6000 + f, 0, 50) for f in range(64)] + [keygen.key16(1, 0, 5000)])
+    assert np.array_equal(ctx.probe(fl, keys, key_len=16), oracle.probe(fl, keys, key_len=16))
+
+
+def test_probe_varlen_keys_sliced(ctx, oracle):
+    fl, _ = _c3_filters(oracle, 8)
+    data, offs = keygen.varlen(100_000)
+    assert np.array_equal(ctx.probe(fl, data, offs), oracle.probe(fl, data, offs))
+
+
+# ---------------------------------------------------------------- device-resident API
+def test_device_api_torch(ctx, oracle):
+    import torch
+    dev = torch.device("cuda:0")
+    n = 1_000_003
+    keys = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+    ctx.gen_key16_dev(0x5EED0001, 0, n, keys)
+    torch.cuda.synchronize()
+    host = keygen.key16(0x5EED0001, 0, n)
+    assert np.array_equal(keys.cpu().numpy(), host)
+    nb, k = lsmbloom.params(n, 0.01)
+    words = torch.zeros(lsmbloom.num_words(nb), dtype=torch.int64, device=dev)
+    ctx.build_fixed_dev(keys, 16, n, nb, k, words)
+    torch.cuda.synchronize()
+    ref = oracle.build_fixed(host, 16, nb, k)
+    _cmp(words.cpu().numpy().view(np.uint64), ref)
+    # unaligned base pointer -> generic fixed-length path
+    raw = torch.zeros(n * 16 + 16, dtype=torch.uint8, device=dev)
+    raw[3:3 + n * 16] = keys.reshape(-1)
+    w2 = torch.zeros_like(words)
+    ctx.build_fixed_dev(raw[3:], 16, n, nb, k, w2)
+    torch.cuda.synchronize()
+    assert torch.equal(words, w2)
+    out = torch.zeros(n, dtype=torch.uint8, device=dev)
+    ctx.probe_dev([(words, nb, k)], keys, n, out, key_len=16)
+    torch.cuda.synchronize()
+    assert bool(out.bool().all())
+
+
+def test_or_reduce_dev(ctx):
+    import torch
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device="cpu").manual_seed(0)
+    src = torch.randint(-2**62, 2**62, (4, 100_001), generator=g, dtype=torch.int64)
+    dst = torch.randint(-2**62, 2**62, (100_001,), generator=g, dtype=torch.int64)
+    ref = dst.clone()
+    for j in range(4):
+        ref |= src[j]
+    d_dst, d_src = dst.to(dev), src.to(dev)
+    ctx.or_reduce_dev(d_dst, d_src, 100_001, 4, 100_001)
+    torch.cuda.synchronize()
+    assert torch.equal(d_dst.cpu(), ref)
+
+
+@pytest.mark.slow
+def test_c2_full_size_bit_exact(ctx, oracle):
+    """BASELINE C2 at full size: 100 M key16 into new(1e8, 0.01), every word."""
+    import torch
+    n = 100_000_000
+    nb, k = lsmbloom.params(n, 0.01)
+    assert (nb, k) == (956_715_292, 7)
+    dev = torch.device("cuda:0")
+    keys = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+    ctx.gen_key16_dev(0x5EED0001, 0, n, keys)
+    words = torch.zeros(lsmbloom.num_words(nb), dtype=torch.int64, device=dev)
+    ctx.build_fixed_dev(keys, 16, n, nb, k, words)
+    torch.cuda.synchronize()
+    got = words.cpu().numpy().view(np.uint64)
+    del keys
+    host = oracle.key16(0x5EED0001, 0, n)
+    ref = oracle.build_fixed_mt(host, 16, nb, k, 16)
+    _cmp(got, ref)
