@@ -15,15 +15,17 @@
 //              builds a private copy with ds_or, then ORs non-zero words into
 //              HBM with one global atomic per word.
 //   Partition  big filters (BASELINE C2/C5: 120 MB / 512 MiB): two passes.
-//              Pass A hashes a tile of keys, counting-sorts its k*tile
-//              positions by 2^20-bit slice in LDS, reserves one run per
-//              (tile, slice) with a single global atomic and writes the run
-//              contiguously.  Pass B gives each slice to one workgroup, which
-//              pulls the slice's words into 128 KiB of LDS, applies every
-//              position with ds_or, and writes the slice back once.  No
-//              random global atomics on the filter (the memory-side atomic
-//              unit serves ~20 G scattered requests/s chip-wide; 7e8 of them
-//              would take ~35 ms at C2).
+//              Pass A hashes keys and appends each position's 20-bit offset
+//              within its 2^20-bit slice to a per-slice 64-B segment buffer
+//              in LDS (3 offsets per u64, ds_or_b64); every full segment is
+//              flushed with whole-segment stores into the workgroup's private
+//              region for that slice (no global atomics, no partial-line
+//              writes, 2.67 B per position instead of 4).  Pass B gives each
+//              slice to one workgroup, which pulls the slice's words into
+//              128 KiB of LDS, applies every offset from every region with
+//              ds_or, and writes the slice back once.  No random global
+//              atomics on the filter (the memory-side atomic unit serves ~20 G
+//              scattered requests/s chip-wide; 7e8 of them would take ~35 ms).
 //   Atomic     few keys into a huge filter: direct global atomicOr.
 #include "kernels.hpp"
 #include "keysrc.hpp"
@@ -79,140 +81,279 @@ __global__ __launch_bounds__(256) void k_build_atomic(Src src, uint64_t n, Mod32
 }
 
 // ---------------------------------------------------------------- Partition strategy
-// Exclusive scan of a[0..nb) in place (LDS); returns the total.  tmp holds
-// one word per wave plus the total.
-template <int BLOCK>
-__device__ uint32_t block_scan_inplace(uint32_t* a, uint32_t nb, uint32_t* tmp) {
-    constexpr int NW = BLOCK / 64;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t per = (nb + BLOCK - 1) / BLOCK;
-    const uint32_t s = min(tid * per, nb), e = min(s + per, nb);
-    uint32_t sum = 0;
-    for (uint32_t b = s; b < e; b++) sum += a[b];
-    uint32_t x = sum;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        uint32_t y = __shfl_up(x, off, 64);
-        if (lane >= (uint32_t)off) x += y;
+struct PassA {
+    uint32_t b0, nb;        // this sweep's slices [b0, b0 + nb)
+    uint32_t grid, cap;     // regions per slice, region capacity (segments)
+    uint64_t* regions;      // [nbins][grid][cap][8] u64
+    uint32_t* counts;       // [nbins][grid] segments written
+    uint32_t* gw;           // filter words (overflow fallback only)
+    uint32_t* err;          // set to 1 if a bounded wait ever times out (a bug; never expected)
+};
+
+// Every wait in pass A is bounded: a protocol bug must surface as an error
+// (LSMB_EHIP at the next sync), never as a hung GPU.
+#ifndef LSMB_SPIN_LIMIT
+#define LSMB_SPIN_LIMIT (1u << 22)
+#endif
+constexpr uint32_t kSpinLimit = LSMB_SPIN_LIMIT;
+
+// Exponential backoff for every wait in pass A: pollers must not crowd the
+// LDS that the lanes they wait for need (64 * 2^j clocks, j <= 5).
+__device__ __forceinline__ void backoff(uint32_t spin) {
+    switch (spin < 5 ? spin : 5) {
+        case 0: __builtin_amdgcn_s_sleep(1); break;
+        case 1: __builtin_amdgcn_s_sleep(2); break;
+        case 2: __builtin_amdgcn_s_sleep(4); break;
+        case 3: __builtin_amdgcn_s_sleep(8); break;
+        case 4: __builtin_amdgcn_s_sleep(16); break;
+        default: __builtin_amdgcn_s_sleep(32); break;
     }
-    if (lane == 63) tmp[wave] = x;
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t run = 0;
-        for (int w = 0; w < NW; w++) {
-            uint32_t t = tmp[w];
-            tmp[w] = run;
-            run += t;
-        }
-        tmp[NW] = run;
-    }
-    __syncthreads();
-    uint32_t excl = tmp[wave] + x - sum;
-    for (uint32_t b = s; b < e; b++) {
-        uint32_t v = a[b];
-        a[b] = excl;
-        excl += v;
-    }
-    __syncthreads();
-    return tmp[NW];
 }
 
-// Pass A: hash + bin.  KPT keys per thread per tile, at most KMAX hashes each.
-template <class Src, int KMAX, int KPT>
-__global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md, uint32_t k,
-                                                   uint32_t nbins, uint32_t cap,
-                                                   uint32_t* __restrict__ bins,
-                                                   uint32_t* __restrict__ cursor,
-                                                   uint32_t* __restrict__ gw) {
-    extern __shared__ uint32_t smem[];
-    uint32_t* hist = smem;            // counts, then exclusive offsets (lbase)
-    uint32_t* gbase = hist + nbins;   // global run start per slice
-    uint32_t* tmp = gbase + nbins;    // scan scratch (32 words)
-    uint32_t* stage = tmp + 32;       // kBinBlock*KPT*k positions, slice-sorted
-    const uint32_t tid = threadIdx.x;
-    constexpr uint64_t TILE = (uint64_t)kBinBlock * KPT;
-    const uint64_t ntiles = (n + TILE - 1) / TILE;
+__device__ __forceinline__ uint64_t* region_ptr(const PassA& a, uint32_t b, uint32_t w) {
+    return a.regions + ((uint64_t)b * a.grid + w) * a.cap * kSegWords;
+}
 
-    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        for (uint32_t b = tid; b < nbins; b += kBinBlock) hist[b] = 0;
-        __syncthreads();
-        uint32_t pos[KPT][KMAX], slot[KPT][KMAX];
-        const uint64_t base = t * TILE;
+// LDS accessors through address_space(3) pointers, so every access in the
+// protocol is a DS instruction (a wave's DS operations execute in issue
+// order); a plain generic pointer would compile to FLAT accesses, which are
+// slower and complete out of order.
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) u32x4 lds_v4;
+
+__device__ __forceinline__ lds_u32* to_lds(uint32_t* p) { return (lds_u32*)p; }
+__device__ __forceinline__ uint32_t lds_load_volatile(const uint32_t* p) { return *(volatile lds_u32*)(lds_u32*)(p); }
+__device__ __forceinline__ void lds_store_volatile(uint32_t* p, uint32_t v) { *(volatile lds_u32*)to_lds(p) = v; }
+
+// Packs 24 offsets into 8 words (3 x 20 bits each) and writes them as
+// segment `seg` of region (b, w); past the region's capacity (adversarial
+// inputs, e.g. one key repeated millions of times) the offsets go straight
+// into the filter with global atomics instead: exact.  `slot(e)` returns
+// offset e.
+template <class SlotFn>
+__device__ __forceinline__ void write_segment(const PassA& a, SlotFn slot, uint32_t b, uint32_t w, uint32_t seg) {
+    if (seg < a.cap) {
+        uint4* dst = reinterpret_cast<uint4*>(region_ptr(a, b, w) + (uint64_t)seg * kSegWords);
 #pragma unroll
-        for (int j = 0; j < KPT; j++) {
-            const uint64_t i = base + (uint64_t)j * kBinBlock + tid;
-            if (i < n) {
-                H128 h = src.hash(i);
-                PosWalk pw(md, h.lo, h.hi);
+        for (int j = 0; j < 4; j++) {
+            const uint64_t w0 = (uint64_t)(slot(6 * j) & kSliceMask) | ((uint64_t)(slot(6 * j + 1) & kSliceMask) << 20) |
+                                ((uint64_t)(slot(6 * j + 2) & kSliceMask) << 40);
+            const uint64_t w1 = (uint64_t)(slot(6 * j + 3) & kSliceMask) |
+                                ((uint64_t)(slot(6 * j + 4) & kSliceMask) << 20) |
+                                ((uint64_t)(slot(6 * j + 5) & kSliceMask) << 40);
+            dst[j] = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+        }
+    } else {
+        for (int e = 0; e < kSegEntries; e++) {
+            const uint32_t p = (b << kSliceLog2) | (slot(e) & kSliceMask);
+            atomicOr(a.gw + (p >> 5), 1u << (p & 31));
+        }
+    }
+}
+
+// LDS state of pass A, per slice of the sweep:
+//   slots[lb][24]  u32 20-bit offsets of the open segment
+//   claims[lb]     slots handed out (>= 24: segment full, claim void)
+//   done[lb]       slots written
+//   cur[lb]        segments this workgroup has written for the slice
+// A lane claims a slot (ds_add_rtn on claims), writes its offset (ds_write),
+// then counts itself in done (ds_add_rtn).  A wave's DS operations execute in
+// issue order, so the lane whose done-increment returns 23 knows all 24
+// offsets are in place: it flushes the segment and re-opens the buffer
+// (done = 0, then claims = 0).  The claim -> write -> done sequence of every
+// valid claim never waits on anything, so re-opens always happen; the only
+// waiting lanes are void claims (buffer full) polling for the re-open.  That
+// matters under SIMT lockstep: a wave's lanes cannot pass a divergent spin
+// loop until all of them can, so no lane may spin on work another lane could
+// be holding back.  Every wait is bounded (err flag) and backs off.
+__device__ __forceinline__ void flush_segment(const PassA& a, uint32_t* slots, uint32_t* claims, uint32_t* done,
+                                              uint32_t* cur, uint32_t lb, uint32_t w) {
+    const volatile lds_v4* sl4 = (const volatile lds_v4*)to_lds(slots + lb * kSegEntries);  // 16-B aligned
+    uint32_t v[kSegEntries];
 #pragma unroll
-                for (int q = 0; q < KMAX; q++) {
-                    if ((uint32_t)q < k) {
-                        pos[j][q] = pw.pos();
-                        slot[j][q] = atomicAdd(&hist[pos[j][q] >> kSliceLog2], 1u);
-                        pw.next(md);
+    for (int j = 0; j < kSegEntries / 4; j++) {
+        const u32x4 x = sl4[j];
+        v[4 * j] = x.x;
+        v[4 * j + 1] = x.y;
+        v[4 * j + 2] = x.z;
+        v[4 * j + 3] = x.w;
+    }
+    const uint32_t c = lds_load_volatile(cur + lb);
+    write_segment(a, [&](int e) { return v[e]; }, a.b0 + lb, w, c);
+    lds_store_volatile(cur + lb, c + 1);
+    lds_store_volatile(done + lb, 0);
+    lds_store_volatile(claims + lb, 0);
+}
+
+// Pass A.  One key per lane per iteration; W = Walk32 when num_bits <= 2^31,
+// else Walk64.  KMAX bounds k: a key's k claims, writes and done-counts are
+// each issued back to back.
+template <class Src, class W, int KMAX>
+__global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md, uint32_t k, PassA a) {
+    extern __shared__ uint32_t smem32[];
+    uint32_t* slots = smem32;                               // nb * 24
+    uint32_t* claims = slots + (size_t)a.nb * kSegEntries;  // nb
+    uint32_t* done = claims + a.nb;                         // nb
+    uint32_t* cur = done + a.nb;                            // nb
+    const uint32_t tid = threadIdx.x, w = blockIdx.x;
+    for (uint32_t i = tid; i < a.nb * (kSegEntries + 3); i += kBinBlock) smem32[i] = 0;
+    __syncthreads();
+
+    // Workgroup w owns keys [w*per, (w+1)*per): a contiguous, coalesced run.
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t i0 = (uint64_t)w * per, i1 = min(n, i0 + per);
+    for (uint64_t i = i0 + tid; i < i1; i += kBinBlock) {
+        const H128 h = src.hash(i);
+        W walk(md, h.lo, h.hi);
+        uint32_t lb[KMAX], off[KMAX], slot[KMAX], dn[KMAX];
+#pragma unroll
+        for (int q = 0; q < KMAX; q++) {
+            lb[q] = 0xFFFFFFFFu;
+            if ((uint32_t)q < k) {
+                const uint32_t p = walk.pos();
+                const uint32_t b = (p >> kSliceLog2) - a.b0;
+                if (b < a.nb) {
+                    lb[q] = b;
+                    off[q] = p & kSliceMask;
+                }
+                walk.next(md);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < KMAX; q++)
+            if (lb[q] != 0xFFFFFFFFu) slot[q] = atomicAdd(&claims[lb[q]], 1u);
+#pragma unroll
+        for (int q = 0; q < KMAX; q++)
+            if (lb[q] != 0xFFFFFFFFu && slot[q] < (uint32_t)kSegEntries)
+                lds_store_volatile(slots + lb[q] * kSegEntries + slot[q], off[q]);
+#pragma unroll
+        for (int q = 0; q < KMAX; q++)
+            if (lb[q] != 0xFFFFFFFFu && slot[q] < (uint32_t)kSegEntries) dn[q] = atomicAdd(&done[lb[q]], 1u);
+        // flushes (wait-free), then retries of void claims: one code path
+        // each, the operands picked out of the unrolled arrays with selects
+        uint32_t fmask = 0, rmask = 0;
+#pragma unroll
+        for (int q = 0; q < KMAX; q++) {
+            if (lb[q] != 0xFFFFFFFFu) {
+                if (slot[q] < (uint32_t)kSegEntries)
+                    fmask |= (uint32_t)(dn[q] == (uint32_t)kSegEntries - 1) << q;
+                else
+                    rmask |= 1u << q;
+            }
+        }
+        while (fmask) {
+            const int qs = __ffs(fmask) - 1;
+            fmask &= fmask - 1;
+            uint32_t L = 0;
+#pragma unroll
+            for (int q = 0; q < KMAX; q++)
+                if (q == qs) L = lb[q];
+            flush_segment(a, slots, claims, done, cur, L, w);
+        }
+        // Retry loop with a WAVE-UNIFORM exit (ballot): every lane's claim,
+        // write, done-count and flush happen inside the iteration that makes
+        // them.  (With a per-lane `break`, the compiler moves the success
+        // path to the loop exit, which a lane only reaches once all its
+        // wave-mates are done: a wave-mate waiting on that very segment then
+        // never sees it complete.)
+        uint32_t idle = 0;
+        for (uint32_t spin = 0; __ballot(rmask != 0); spin++) {
+            if (rmask) {
+                const int qs = __ffs(rmask) - 1;
+                uint32_t L = 0, O = 0;
+#pragma unroll
+                for (int q = 0; q < KMAX; q++)
+                    if (q == qs) {
+                        L = lb[q];
+                        O = off[q];
+                    }
+                if (lds_load_volatile(claims + L) < (uint32_t)kSegEntries) {  // poll before claiming
+                    const uint32_t s1 = atomicAdd(&claims[L], 1u);
+                    if (s1 < (uint32_t)kSegEntries) {
+                        lds_store_volatile(slots + L * kSegEntries + s1, O);
+                        if (atomicAdd(&done[L], 1u) == (uint32_t)kSegEntries - 1)
+                            flush_segment(a, slots, claims, done, cur, L, w);
+                        rmask &= rmask - 1;
                     }
                 }
             }
-        }
-        __syncthreads();
-        const uint32_t total = block_scan_inplace<kBinBlock>(hist, nbins, tmp);
-        for (uint32_t b = tid; b < nbins; b += kBinBlock) {
-            const uint32_t c = (b + 1 < nbins ? hist[b + 1] : total) - hist[b];
-            gbase[b] = c ? atomicAdd(&cursor[b], c) : 0u;
-        }
+            if (spin == kSpinLimit) {
+                if (rmask && atomicOr(a.err, 2u) == 0u) {  // first timeout: dump the stuck slice
+                    const int qs = __ffs(rmask) - 1;
+                    uint32_t L = 0;
 #pragma unroll
-        for (int j = 0; j < KPT; j++) {
-            const uint64_t i = base + (uint64_t)j * kBinBlock + tid;
-            if (i < n) {
-#pragma unroll
-                for (int q = 0; q < KMAX; q++)
-                    if ((uint32_t)q < k) stage[hist[pos[j][q] >> kSliceLog2] + slot[j][q]] = pos[j][q];
+                    for (int q = 0; q < KMAX; q++)
+                        if (q == qs) L = lb[q];
+                    a.err[1] = lds_load_volatile(claims + L);
+                    a.err[2] = lds_load_volatile(done + L);
+                    a.err[3] = lds_load_volatile(cur + L);
+                    a.err[4] = L;
+                }
+                break;
             }
+            backoff(idle++);
         }
-        __syncthreads();
-        for (uint32_t e = tid; e < total; e += kBinBlock) {
-            const uint32_t p = stage[e], b = p >> kSliceLog2;
-            const uint32_t g = gbase[b] + (e - hist[b]);
-            if (g < cap)
-                bins[(uint64_t)b * cap + g] = p;
-            else
-                or_bit_global(gw, p);  // run overflow (e.g. duplicate-heavy input): exact, slower
+    }
+    __syncthreads();
+    // Final partial segments, padded with copies of their first offset
+    // (setting a bit twice is a no-op), then the per-region segment counts.
+    for (uint32_t lb = tid; lb < a.nb; lb += kBinBlock) {
+        const uint32_t f = claims[lb];
+        uint32_t c = cur[lb];
+        if (f) {
+            const uint32_t* sl = slots + lb * kSegEntries;
+            write_segment(a, [&](int e) { return (uint32_t)e < f ? sl[e] : sl[0]; }, a.b0 + lb, w, c);
+            c++;
         }
-        __syncthreads();
+        a.counts[(uint64_t)(a.b0 + lb) * a.grid + w] = min(c, a.cap);
     }
 }
 
 // Pass B: one 2^20-bit slice per workgroup, applied in LDS.
-__global__ __launch_bounds__(kApplyBlock) void k_apply(const uint32_t* __restrict__ bins,
-                                                       const uint32_t* __restrict__ cursor,
-                                                       uint32_t cap, uint32_t nbins,
+__global__ __launch_bounds__(kApplyBlock) void k_apply(const uint64_t* __restrict__ regions,
+                                                       const uint32_t* __restrict__ counts,
+                                                       uint32_t grid, uint32_t cap, uint32_t nbins,
                                                        uint32_t* __restrict__ gw, uint64_t nw32) {
     __shared__ uint32_t filt[kSliceWords32];
-    const uint32_t tid = threadIdx.x;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr uint32_t NWAVE = kApplyBlock / 64;
     for (uint32_t b = blockIdx.x; b < nbins; b += gridDim.x) {
         const uint64_t w0 = (uint64_t)b * kSliceWords32;
         const uint32_t nw = (uint32_t)min((uint64_t)kSliceWords32, nw32 - w0);  // even
         uint2* g2 = reinterpret_cast<uint2*>(gw + w0);
         uint2* f2 = reinterpret_cast<uint2*>(filt);
-        for (uint32_t w = tid; w < nw / 2; w += kApplyBlock) f2[w] = g2[w];
+        for (uint32_t i = tid; i < nw / 2; i += kApplyBlock) f2[i] = g2[i];
         __syncthreads();
-        const uint32_t cnt = min(cursor[b], cap);
-        const uint32_t* src = bins + (uint64_t)b * cap;
-        const uint4* s4 = reinterpret_cast<const uint4*>(src);
-        const uint32_t n4 = cnt >> 2;
-        for (uint32_t e = tid; e < n4; e += kApplyBlock) {
-            const uint4 v = ld_stream16(s4 + e);
-            atomicOr(&filt[(v.x >> 5) & (kSliceWords32 - 1)], 1u << (v.x & 31));
-            atomicOr(&filt[(v.y >> 5) & (kSliceWords32 - 1)], 1u << (v.y & 31));
-            atomicOr(&filt[(v.z >> 5) & (kSliceWords32 - 1)], 1u << (v.z & 31));
-            atomicOr(&filt[(v.w >> 5) & (kSliceWords32 - 1)], 1u << (v.w & 31));
-        }
-        for (uint32_t e = (n4 << 2) + tid; e < cnt; e += kApplyBlock) {
-            const uint32_t p = src[e];
-            atomicOr(&filt[(p >> 5) & (kSliceWords32 - 1)], 1u << (p & 31));
+        for (uint32_t r = wave; r < grid; r += NWAVE) {
+            const uint32_t nseg = counts[(uint64_t)b * grid + r];
+            const uint4* src = reinterpret_cast<const uint4*>(regions + ((uint64_t)b * grid + r) * cap * kSegWords);
+            const uint32_t n16 = nseg * (kSegWords / 2);  // 16-B pieces (2 words, 6 offsets)
+            constexpr uint32_t U = 4;                      // loads in flight per lane
+            for (uint32_t i0 = 0; i0 < n16; i0 += 64 * U) {
+                uint4 v[U];
+#pragma unroll
+                for (uint32_t u = 0; u < U; u++) {
+                    const uint32_t i = i0 + u * 64 + lane;
+                    v[u] = i < n16 ? ld_stream16(src + i) : make_uint4(0, 0, 0, 0);
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < U; u++) {
+                    if (i0 + u * 64 + lane < n16) {
+                        const uint64_t lo = ((uint64_t)v[u].y << 32) | v[u].x;
+                        const uint64_t hi = ((uint64_t)v[u].w << 32) | v[u].z;
+#pragma unroll
+                        for (int e = 0; e < 3; e++) {
+                            const uint32_t o0 = (uint32_t)(lo >> (20 * e)) & kSliceMask;
+                            const uint32_t o1 = (uint32_t)(hi >> (20 * e)) & kSliceMask;
+                            atomicOr(&filt[o0 >> 5], 1u << (o0 & 31));
+                            atomicOr(&filt[o1 >> 5], 1u << (o1 & 31));
+                        }
+                    }
+                }
+            }
         }
         __syncthreads();
-        for (uint32_t w = tid; w < nw / 2; w += kApplyBlock) g2[w] = f2[w];
+        for (uint32_t i = tid; i < nw / 2; i += kApplyBlock) g2[i] = f2[i];
         __syncthreads();
     }
 }
@@ -270,37 +411,37 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
         k_build_atomic<Src><<<dim3((uint32_t)g), dim3(256), 0, st>>>(src, n, md, k, gw);
         if (tm) hipEventRecord(tm->t1, st);
     } else {
-        uint32_t nbins, cap;
-        partition_sizing(num_bits, k, n, &nbins, &cap);
-        if ((uint64_t)nbins * cap > ws.entries || nbins > ws.nbins_cap) return hipErrorInvalidValue;
-        hipError_t e = hipMemsetAsync(ws.cursor, 0, (size_t)nbins * 4, st);
-        if (e != hipSuccess) return e;
-        const void* fn;
-        size_t smem;
-        auto launch = [&](auto kern, int kmax, int kp) {
-            smem = ((size_t)2 * nbins + 32 + (size_t)kBinBlock * kp * k) * 4;
-            fn = (const void*)kern;
-            (void)kmax;
-            hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-            int per_cu = 0;
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kBinBlock, smem);
-            if (per_cu < 1) per_cu = 1;
-            const uint64_t tile = (uint64_t)kBinBlock * kp;
-            uint64_t g = (n + tile - 1) / tile, gmax = (uint64_t)num_cus * per_cu;
-            if (g > gmax) g = gmax;
-            kern<<<dim3((uint32_t)g), dim3(kBinBlock), smem, st>>>(src, n, md, k, nbins, cap, ws.bins,
-                                                                ws.cursor, gw);
-        };
-        if (k <= 8)
-            launch(k_bin<Src, 8, 4>, 8, 4);
-        else if (k <= 16)
-            launch(k_bin<Src, 16, 2>, 16, 2);
-        else
-            launch(k_bin<Src, 32, 1>, 32, 1);
-        e = hipGetLastError();
-        if (e != hipSuccess) return e;
+        const PartitionPlan pl = plan_partition(num_bits, k, n, num_cus);
+        if (pl.region_bytes > ws.region_bytes || pl.counts_bytes > ws.counts_bytes) return hipErrorInvalidValue;
+        const bool w32 = fits_walk32(num_bits);
+        for (uint32_t sw = 0; sw < pl.sweeps; sw++) {
+            PassA a;
+            a.b0 = sw * pl.bins_per_sweep;
+            a.nb = min(pl.bins_per_sweep, pl.nbins - a.b0);
+            a.grid = pl.grid;
+            a.cap = pl.cap_segs;
+            a.regions = ws.regions;
+            a.counts = ws.counts;
+            a.gw = gw;
+            a.err = ws.err;
+            const size_t smem = (size_t)a.nb * kLdsBytesPerBin;
+            auto go = [&](auto kern) {
+                hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+                kern<<<dim3(pl.grid), dim3(kBinBlock), smem, st>>>(src, n, md, k, a);
+            };
+            if (k <= 8) {
+                if (w32) go(k_bin<Src, Walk32, 8>); else go(k_bin<Src, Walk64, 8>);
+            } else if (k <= 16) {
+                if (w32) go(k_bin<Src, Walk32, 16>); else go(k_bin<Src, Walk64, 16>);
+            } else {
+                if (w32) go(k_bin<Src, Walk32, 32>); else go(k_bin<Src, Walk64, 32>);
+            }
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
         if (tm) hipEventRecord(tm->t1, st);
-        k_apply<<<dim3(nbins), dim3(kApplyBlock), 0, st>>>(ws.bins, ws.cursor, cap, nbins, gw, nw32);
+        k_apply<<<dim3(pl.nbins), dim3(kApplyBlock), 0, st>>>(ws.regions, ws.counts, pl.grid, pl.cap_segs,
+                                                              pl.nbins, gw, nw32);
     }
     if (tm) {
         hipEventRecord(tm->t2, st);
@@ -328,29 +469,44 @@ BuildStrategy pick_build_strategy(uint32_t num_bits, uint32_t k, uint64_t n) {
     if (k > 32) return BuildStrategy::Atomic;
     // Few keys into a big filter: scattered atomics beat a full-slice RMW.
     if (n * (uint64_t)k < nw32 / 16) return BuildStrategy::Atomic;
+    // Fewer than 64 slices (< 8 MiB filters): too few LDS buffers to spread
+    // a workgroup's claims; memory-side atomics on the small filter instead.
+    if (nw32 < 64ull * kSliceWords32) return BuildStrategy::Atomic;
     return BuildStrategy::Partition;
 }
 
-void partition_sizing(uint32_t num_bits, uint32_t k, uint64_t n, uint32_t* nbins, uint32_t* cap) {
-    const uint64_t nb = ((uint64_t)num_bits + (1ull << kSliceLog2) - 1) >> kSliceLog2;
-    const double p = (double)(1ull << kSliceLog2) / (double)num_bits;
-    const double mu = (double)n * k * (p > 1.0 ? 1.0 : p);
-    double c = mu + 8.0 * sqrt(mu) + 64.0;
-    uint64_t ci = (uint64_t)c;
-    ci = (ci + 3) & ~3ull;
-    if (ci > 0xFFFFFFF0ull) ci = 0xFFFFFFF0ull;
-    *nbins = (uint32_t)nb;
-    *cap = (uint32_t)ci;
+PartitionPlan plan_partition(uint32_t num_bits, uint32_t k, uint64_t n, int num_cus) {
+    PartitionPlan pl;
+    pl.nbins = (uint32_t)(((uint64_t)num_bits + kSliceMask) >> kSliceLog2);
+    // <= 1536 slices per sweep keeps a pass A workgroup within 150 KiB of
+    // LDS (one 1024-thread workgroup per CU); bigger filters take more sweeps
+    // (each re-reads and re-hashes the keys, and keeps only its slices).
+    pl.sweeps = (pl.nbins + kMaxBinsPerSweep - 1) / kMaxBinsPerSweep;
+    pl.bins_per_sweep = (pl.nbins + pl.sweeps - 1) / pl.sweeps;
+    const uint32_t per_cu = pl.bins_per_sweep * kLdsBytesPerBin <= 80 * 1024 ? 2 : 1;
+    // at least ~kBinBlock keys per workgroup
+    const uint64_t gmax = (n + kBinBlock - 1) / kBinBlock;
+    uint64_t g = (uint64_t)num_cus * per_cu;
+    if (g > gmax) g = gmax;
+    if (g < 1) g = 1;
+    pl.grid = (uint32_t)g;
+    const uint64_t keys_w = (n + g - 1) / g;  // workgroup w hashes keys [w*keys_w, (w+1)*keys_w)
+    double p = (double)(1u << kSliceLog2) / (double)num_bits;
+    if (p > 1.0) p = 1.0;
+    const double mu = (double)keys_w * k * p;
+    const double cap_e = mu + 8.0 * sqrt(mu) + 2.0 * kSegEntries;
+    pl.cap_segs = (uint32_t)ceil(cap_e / kSegEntries);
+    pl.region_bytes = (uint64_t)pl.nbins * pl.grid * pl.cap_segs * 64;
+    pl.counts_bytes = (uint64_t)pl.nbins * pl.grid * 4;
+    return pl;
 }
 
-uint64_t partition_chunk_keys(uint32_t num_bits, uint32_t k, uint64_t max_entries) {
-    if (k == 0) return ~0ull;
-    uint64_t hi = max_entries / k + 1, lo = 0;
-    while (lo + 1 < hi) {  // largest n with nbins*cap <= max_entries
-        uint64_t mid = lo + (hi - lo) / 2;
-        uint32_t nb, cap;
-        partition_sizing(num_bits, k, mid, &nb, &cap);
-        if ((uint64_t)nb * cap <= max_entries) lo = mid; else hi = mid;
+uint64_t partition_chunk_keys(uint32_t num_bits, uint32_t k, uint64_t max_bytes, int num_cus) {
+    uint64_t lo = 0, hi = (1ull << 40);
+    while (lo + 1 < hi) {  // largest n whose plan fits
+        const uint64_t mid = lo + (hi - lo) / 2;
+        const PartitionPlan pl = plan_partition(num_bits, k, mid, num_cus);
+        if (pl.region_bytes + pl.counts_bytes <= max_bytes) lo = mid; else hi = mid;
     }
     return lo;
 }

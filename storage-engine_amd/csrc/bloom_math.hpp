@@ -6,67 +6,105 @@
 // has no integer divider, so a literal `%` is a long software sequence per
 // position.  We evaluate the same integers with:
 //
-//   * one exact reduction per key for h1 and for h2 (`Mod32::reduce`): a
-//     64-bit reciprocal m = floor((2^64-1)/d) gives q' = mulhi(x, m) in
-//     {q-1, q}, so r = x - q'd needs at most one conditional subtract;
+//   * one exact reduction per key for h1 and for h2 (`Mod32::reduce`):
+//       y = hi32(x) * (2^32 mod d) + lo32(x)        (one v_mad_u64_u32; y < d*2^32)
+//       q = (u32)(f64(y) * f64(1/d))                (|q - floor(y/d)| <= 1, see below)
+//       r = y - q*d, then one fix-up each way.
+//     f64(y) is exact when y < 2^53 and otherwise off by at most
+//     y*2^-53 < d*2^-21, so y/d is known to within 2^-21 + 2^-20 and the
+//     truncated quotient is off by at most one;
 //   * a strength-reduced walk over i: x_i = x_{i-1} + h2 (mod 2^64) with carry
-//     c_i, hence x_i mod d = (r_{i-1} + (h2 mod d) - c_i * (2^64 mod d)) mod d,
-//     which costs a 64-bit add, a carry test and two conditional fix-ups.
+//     c_i, hence x_i mod d = (r_{i-1} + (h2 mod d) - c_i * (2^64 mod d)) mod d.
+//     For d <= 2^31 every intermediate fits 32 bits (`Walk32`), and each
+//     "mod d" fix-up is a subtract and an unsigned min.
 //
-// Both are exact for every d in [1, 2^32); tests/test_host_logic.py checks
-// them against the oracle's literal `%` on random and edge-case inputs.
+// The host compiles the very same code (fma() matches v_fma_f64), and
+// tests/test_capi_host.py checks it against the oracle's literal `%` over
+// random and edge-case moduli in [1, 2^32).
 #pragma once
+
+#include <math.h>
 
 #include "xxh3.hpp"
 
 namespace lsmb {
 
 struct Mod32 {
-    uint64_t d;     // divisor (num_bits), 1 <= d < 2^32
-    uint64_t m;     // floor((2^64 - 1) / d)
-    uint64_t t;     // 2^64 mod d
+    uint32_t d;     // divisor (num_bits), 1 <= d < 2^32
+    uint32_t t32;   // 2^32 mod d
+    uint32_t t64;   // 2^64 mod d
+    uint32_t dt;    // d - t64 (in (0, d])
+    double inv;     // 1.0 / d
 
     static Mod32 make(uint32_t d32) {
         Mod32 r;
         r.d = d32;
-        r.m = ~0ULL / r.d;
-        r.t = (~0ULL % r.d + 1) % r.d;
+        r.t32 = (uint32_t)((1ull << 32) % d32);
+        r.t64 = (uint32_t)((uint64_t)(((unsigned __int128)1 << 64) % d32));
+        r.dt = d32 - r.t64;
+        r.inv = 1.0 / (double)d32;
         return r;
     }
 
-    LSMB_HD uint64_t reduce(uint64_t x) const {
-#ifdef __HIP_DEVICE_COMPILE__
-        uint64_t q = __umul64hi(x, m);
-#else
-        uint64_t q = (uint64_t)(((unsigned __int128)x * m) >> 64);
-#endif
-        uint64_t r = x - q * d;
-        return r >= d ? r - d : r;
+    LSMB_HD uint32_t reduce(uint64_t x) const {
+        const uint64_t y = (uint64_t)(uint32_t)(x >> 32) * t32 + (uint32_t)x;
+        const double yd = fma((double)(uint32_t)(y >> 32), 4294967296.0, (double)(uint32_t)y);
+        const double qd = yd * inv;
+        const uint32_t q = qd >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)qd;
+        int64_t r = (int64_t)(y - (uint64_t)q * d);
+        if (r < 0) r += d;
+        if (r >= (int64_t)d) r -= d;
+        return (uint32_t)r;
     }
 };
 
-// Walks the k positions of one key in order i = 0, 1, ..., k-1.
-struct PosWalk {
-    uint64_t x;     // h1 + i*h2 (mod 2^64)
-    uint64_t h2;
-    uint64_t r;     // x mod d
-    uint64_t s;     // h2 mod d
+// k positions of one key, i = 0, 1, ..., for d <= 2^31 (all sums fit 32 bits).
+struct Walk32 {
+    uint64_t x, h2;
+    uint32_t r, s;
 
-    LSMB_HD PosWalk(const Mod32& md, uint64_t h1, uint64_t h2_) : x(h1), h2(h2_) {
+    LSMB_HD Walk32(const Mod32& md, uint64_t h1, uint64_t h2_) : x(h1), h2(h2_) {
         r = md.reduce(h1);
         s = md.reduce(h2_);
     }
-    LSMB_HD uint32_t pos() const { return (uint32_t)r; }
+    LSMB_HD uint32_t pos() const { return r; }
     LSMB_HD void next(const Mod32& md) {
-        uint64_t nx = x + h2;
-        bool carry = nx < x;
+        uint64_t nx;
+        const bool carry = __builtin_add_overflow(x, h2, &nx);
         x = nx;
-        uint64_t u = r + s;
-        if (u >= md.d) u -= md.d;
-        if (carry) u = (u >= md.t) ? u - md.t : u + md.d - md.t;
-        r = u;
+        uint32_t u = r + s;
+        u = u - md.d < u ? u - md.d : u;           // (r + s) mod d
+        uint32_t w = u + md.dt;
+        w = w - md.d < w ? w - md.d : w;           // (u - 2^64 mod d) mod d
+        r = carry ? w : u;
     }
 };
+
+// The same walk for any d < 2^32 (64-bit intermediate sums).
+struct Walk64 {
+    uint64_t x, h2;
+    uint32_t r, s;
+
+    LSMB_HD Walk64(const Mod32& md, uint64_t h1, uint64_t h2_) : x(h1), h2(h2_) {
+        r = md.reduce(h1);
+        s = md.reduce(h2_);
+    }
+    LSMB_HD uint32_t pos() const { return r; }
+    LSMB_HD void next(const Mod32& md) {
+        uint64_t nx;
+        const bool carry = __builtin_add_overflow(x, h2, &nx);
+        x = nx;
+        uint64_t u = (uint64_t)r + s;
+        if (u >= md.d) u -= md.d;
+        if (carry) u = (u >= md.t64) ? u - md.t64 : u + md.dt;
+        r = (uint32_t)u;
+    }
+};
+
+// The 64-bit-safe walk, used where d may exceed 2^31.
+using PosWalk = Walk64;
+
+LSMB_HD bool fits_walk32(uint32_t d) { return d <= 0x80000000u; }
 
 // BloomFilter::new sizing (src/bloom/mod.rs:38-67), host only.  Returns false
 // where the reference panics (expected_items == 0, fpr outside (0, 1)).

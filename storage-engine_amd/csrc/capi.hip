@@ -76,11 +76,11 @@ struct DevBuf {
     }
 };
 
-uint64_t workspace_limit_entries() {
+uint64_t workspace_limit_bytes() {
     const char* s = getenv("LSMB_WORKSPACE_MB");
     uint64_t mb = s ? strtoull(s, nullptr, 10) : 8192;
     if (mb < 16) mb = 16;
-    return mb * (1ull << 20) / 4;
+    return mb << 20;
 }
 
 }  // namespace
@@ -90,7 +90,9 @@ struct lsmb_ctx {
     int num_cus = 256;
     hipStream_t st = nullptr;
     BuildTimers tm;
-    DevBuf ws_bins, ws_cursor;     // partition workspace
+    DevBuf ws_regions, ws_counts;  // partition workspace
+    DevBuf err;                    // device error flag of the partition kernels
+    uint32_t* err_host = nullptr;  // pinned mirror read at sync
     DevBuf keys, offs, words, out; // staging for the host-memory entry points
     DevBuf filt_words;             // probe: device copies of host filters
     DevBuf filt_desc;              // probe: ProbeFilter array
@@ -120,6 +122,20 @@ hipStream_t pick_stream(lsmb_ctx* c, void* stream) {
     return stream ? reinterpret_cast<hipStream_t>(stream) : c->st;
 }
 
+// Reads (and clears) the kernels' device error flag.  Requires the work that
+// could set it to have completed.
+int check_device_error(lsmb_ctx* c) {
+    HIP_TRY(hipMemcpy(c->err_host, c->err.p, 32, hipMemcpyDeviceToHost));
+    if (*c->err_host) {
+        uint32_t e[8];
+        memcpy(e, c->err_host, 32);
+        HIP_TRY(hipMemset(c->err.p, 0, 32));
+        return fail(LSMB_EHIP, "partition build: bounded wait timed out (internal error, code %u, diag %u %u %u %u)",
+                    e[0], e[1], e[2], e[3], e[4]);
+    }
+    return LSMB_OK;
+}
+
 // Device build of one batch, chunked so the partition workspace stays bounded.
 int build_dev(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k, uint32_t* dw,
               hipStream_t st) {
@@ -130,19 +146,18 @@ int build_dev(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k
         HIP_TRY(launch_build(kb_all, num_bits, k, dw, s, PartitionWorkspace{}, c->num_cus, st, &c->tm));
         return LSMB_OK;
     }
-    const uint64_t limit = workspace_limit_entries();
-    uint64_t chunk = partition_chunk_keys(num_bits, k, limit);
+    uint64_t chunk = partition_chunk_keys(num_bits, k, workspace_limit_bytes(), c->num_cus);
     if (chunk == 0) return fail(LSMB_ENOMEM, "partition workspace limit too small");
     chunk = std::min(chunk, kb_all.n);
-    uint32_t nbins, cap;
-    partition_sizing(num_bits, k, chunk, &nbins, &cap);
-    HIP_TRY(c->ws_bins.ensure((size_t)nbins * cap * 4));
-    HIP_TRY(c->ws_cursor.ensure((size_t)nbins * 4));
+    const PartitionPlan pl = plan_partition(num_bits, k, chunk, c->num_cus);
+    HIP_TRY(c->ws_regions.ensure(pl.region_bytes));
+    HIP_TRY(c->ws_counts.ensure(pl.counts_bytes));
     PartitionWorkspace ws;
-    ws.bins = (uint32_t*)c->ws_bins.p;
-    ws.cursor = (uint32_t*)c->ws_cursor.p;
-    ws.entries = c->ws_bins.bytes / 4;
-    ws.nbins_cap = (uint32_t)(c->ws_cursor.bytes / 4);
+    ws.regions = (uint64_t*)c->ws_regions.p;
+    ws.counts = (uint32_t*)c->ws_counts.p;
+    ws.err = (uint32_t*)c->err.p;
+    ws.region_bytes = c->ws_regions.bytes;
+    ws.counts_bytes = c->ws_counts.bytes;
     for (uint64_t first = 0; first < kb_all.n; first += chunk) {
         KeyBatch kb = kb_all;
         kb.n = std::min(chunk, kb_all.n - first);
@@ -153,6 +168,26 @@ int build_dev(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k
         HIP_TRY(launch_build(kb, num_bits, k, dw, s, ws, c->num_cus, st, &c->tm));
     }
     return LSMB_OK;
+}
+
+// Host single-key walks (the same arithmetic the kernels run).
+template <class W, class F>
+void walk_key(const uint8_t* key, uint64_t len, uint32_t num_bits, uint32_t k, F&& f) {
+    const Mod32 md = Mod32::make(num_bits);
+    const H128 h = xxh3_128(key, len);
+    W w(md, h.lo, h.hi);
+    for (uint32_t i = 0; i < k; i++) {
+        if (!f(w.pos())) return;
+        w.next(md);
+    }
+}
+
+template <class F>
+void for_positions(const uint8_t* key, uint64_t len, uint32_t num_bits, uint32_t k, F&& f) {
+    if (fits_walk32(num_bits))
+        walk_key<Walk32>(key, len, num_bits, k, f);
+    else
+        walk_key<Walk64>(key, len, num_bits, k, f);
 }
 
 }  // namespace
@@ -234,44 +269,31 @@ int lsmb_deserialize(const uint8_t* data, uint64_t len, uint64_t* words, uint64_
 
 int lsmb_positions(const uint8_t* key, uint64_t len, uint32_t num_bits, uint32_t k, uint32_t* out) {
     if (int rc = check_filter(num_bits, k)) return rc;
-    if (!k) return LSMB_OK;
-    const Mod32 md = Mod32::make(num_bits);
-    const H128 h = xxh3_128(key, len);
-    PosWalk pw(md, h.lo, h.hi);
-    for (uint32_t i = 0; i < k; i++) {
-        out[i] = pw.pos();
-        pw.next(md);
-    }
+    uint32_t i = 0;
+    if (k) for_positions(key, len, num_bits, k, [&](uint32_t p) { out[i++] = p; return true; });
     return LSMB_OK;
 }
 
 int lsmb_insert(uint64_t* words, uint32_t num_bits, uint32_t k, const uint8_t* key, uint64_t len) {
     if (int rc = check_filter(num_bits, k)) return rc;
-    if (!k) return LSMB_OK;
-    const Mod32 md = Mod32::make(num_bits);
-    const H128 h = xxh3_128(key, len);
-    PosWalk pw(md, h.lo, h.hi);
-    for (uint32_t i = 0; i < k; i++) {
-        const uint32_t p = pw.pos();
-        words[p >> 6] |= 1ull << (p & 63);
-        pw.next(md);
-    }
+    if (k)
+        for_positions(key, len, num_bits, k, [&](uint32_t p) {
+            words[p >> 6] |= 1ull << (p & 63);
+            return true;
+        });
     return LSMB_OK;
 }
 
 int lsmb_may_contain(const uint64_t* words, uint32_t num_bits, uint32_t k, const uint8_t* key,
                      uint64_t len) {
     if (int rc = check_filter(num_bits, k)) return rc;
-    if (!k) return 1;
-    const Mod32 md = Mod32::make(num_bits);
-    const H128 h = xxh3_128(key, len);
-    PosWalk pw(md, h.lo, h.hi);
-    for (uint32_t i = 0; i < k; i++) {
-        const uint32_t p = pw.pos();
-        if (!((words[p >> 6] >> (p & 63)) & 1)) return 0;
-        pw.next(md);
-    }
-    return 1;
+    bool all = true;  // k == 0: the reference's k-loop is empty -> true
+    if (k)
+        for_positions(key, len, num_bits, k, [&](uint32_t p) {
+            all = (words[p >> 6] >> (p & 63)) & 1;
+            return all;  // early exit on the first clear bit (mod.rs:88-90)
+        });
+    return all ? 1 : 0;
 }
 
 int lsmb_open(lsmb_ctx** out, int device) {
@@ -298,6 +320,11 @@ int lsmb_open(lsmb_ctx** out, int device) {
         delete c;
         return fail(LSMB_ENODEV, "stream/event creation failed on device %d", device);
     }
+    if (c->err.ensure(64) != hipSuccess || hipMemset(c->err.p, 0, 64) != hipSuccess ||
+        hipHostMalloc((void**)&c->err_host, 64, 0) != hipSuccess) {
+        lsmb_close(c);
+        return fail(LSMB_ENOMEM, "error-flag allocation failed on device %d", device);
+    }
     *out = c;
     return LSMB_OK;
 }
@@ -307,7 +334,8 @@ void lsmb_close(lsmb_ctx* c) {
     {
         DevGuard g(c->dev);
         hipStreamSynchronize(c->st);
-        for (DevBuf* b : {&c->ws_bins, &c->ws_cursor, &c->keys, &c->offs, &c->words, &c->out,
+        if (c->err_host) hipHostFree(c->err_host);
+        for (DevBuf* b : {&c->ws_regions, &c->ws_counts, &c->err, &c->keys, &c->offs, &c->words, &c->out,
                           &c->filt_words, &c->filt_desc})
             b->release();
         hipEventDestroy(c->tm.t0);
@@ -324,7 +352,7 @@ int lsmb_sync(lsmb_ctx* c) {
     if (!c) return fail(LSMB_EINVAL, "null ctx");
     DevGuard g(c->dev);
     HIP_TRY(hipStreamSynchronize(c->st));
-    return LSMB_OK;
+    return check_device_error(c);
 }
 
 int lsmb_build_fixed_dev(lsmb_ctx* c, const void* d_keys, uint32_t key_len, uint64_t n,
@@ -377,7 +405,7 @@ int lsmb_build_fixed(lsmb_ctx* c, const uint8_t* keys, uint32_t key_len, uint64_
     }
     HIP_TRY(hipMemcpyAsync(words, c->words.p, nw * 8, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(hipStreamSynchronize(c->st));
-    return LSMB_OK;
+    return check_device_error(c);
 }
 
 int lsmb_build_var(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, uint64_t n,
@@ -411,7 +439,7 @@ int lsmb_build_var(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, ui
     }
     HIP_TRY(hipMemcpyAsync(words, c->words.p, nw * 8, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(hipStreamSynchronize(c->st));
-    return LSMB_OK;
+    return check_device_error(c);
 }
 
 static int probe_common(lsmb_ctx* c, const uint32_t* const* wptrs, const uint32_t* filt_bits,
@@ -424,7 +452,7 @@ static int probe_common(lsmb_ctx* c, const uint32_t* const* wptrs, const uint32_
         ProbeFilter& p = c->hfilt[f];
         memset(&p, 0, sizeof p);
         p.words32 = wptrs[f];
-        p.md = filt_bits[f] ? Mod32::make(filt_bits[f]) : Mod32{1, ~0ull, 0};
+        p.md = Mod32::make(filt_bits[f] ? filt_bits[f] : 1);
         p.num_bits = filt_bits[f];
         p.k = filt_k[f];
         p.out_bit = f;

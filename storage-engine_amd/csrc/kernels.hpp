@@ -11,9 +11,14 @@ namespace lsmb {
 // Geometry of the partitioned build (see DESIGN.md "Build kernels").
 constexpr int kSliceLog2 = 20;                        // 2^20 bits = 128 KiB LDS slice
 constexpr uint32_t kSliceWords32 = 1u << (kSliceLog2 - 5);
-constexpr int kBinBlock = 512;                        // pass A workgroup
+constexpr uint32_t kSliceMask = (1u << kSliceLog2) - 1;
+constexpr int kSegEntries = 24;                       // 20-bit offsets per 64-B segment
+constexpr int kSegWords = 8;                          // 3 offsets per u64 word
+constexpr int kBinBlock = 1024;                       // pass A workgroup
 constexpr int kApplyBlock = 1024;                     // pass B workgroup
 constexpr uint32_t kLdsFilterMaxWords32 = 40 * 1024;  // 160 KiB: whole filter in LDS
+constexpr uint32_t kLdsBytesPerBin = kSegEntries * 4 + 12;  // 24 slots + claims/done/cursor
+constexpr uint32_t kMaxBinsPerSweep = 1400;                // 151 KiB of pass A LDS
 
 // How a key batch is presented to the kernels.
 struct KeyBatch {
@@ -28,26 +33,41 @@ enum class BuildStrategy { None, Lds, Partition, Atomic };
 BuildStrategy pick_build_strategy(uint32_t num_bits, uint32_t k, uint64_t n);
 const char* strategy_name(BuildStrategy s);
 
-struct PartitionWorkspace {
-    uint32_t* bins = nullptr;    // nbins * cap entries
-    uint32_t* cursor = nullptr;  // nbins counters
-    uint64_t entries = 0;        // capacity of `bins` in entries
-    uint32_t nbins_cap = 0;      // capacity of `cursor`
+// Partitioned build layout for one chunk of keys.  Pass A workgroup w writes
+// the 20-bit slice offsets of its keys' positions that fall in slice b into
+// its private region (b, w) as 64-B segments; pass B reads every region of
+// slice b.  No global atomics: each region has one writer.
+struct PartitionPlan {
+    uint32_t nbins = 0;           // ceil(num_bits / 2^20)
+    uint32_t grid = 0;            // pass A workgroups = regions per slice
+    uint32_t cap_segs = 0;        // region capacity, segments
+    uint32_t bins_per_sweep = 0;  // slices buffered in LDS per pass A launch
+    uint32_t sweeps = 0;
+    uint64_t region_bytes = 0;    // nbins * grid * cap_segs * 64
+    uint64_t counts_bytes = 0;    // nbins * grid * 4
 };
 
-// Workspace the partitioned build needs for `n` keys (entries, counters).
-void partition_sizing(uint32_t num_bits, uint32_t k, uint64_t n, uint32_t* nbins, uint32_t* cap);
+PartitionPlan plan_partition(uint32_t num_bits, uint32_t k, uint64_t n, int num_cus);
 
-// Largest key count a workspace of `entries` entries can take in one chunk.
-uint64_t partition_chunk_keys(uint32_t num_bits, uint32_t k, uint64_t max_entries);
+// Largest key count whose plan fits `max_bytes` of workspace.
+uint64_t partition_chunk_keys(uint32_t num_bits, uint32_t k, uint64_t max_bytes, int num_cus);
+
+struct PartitionWorkspace {
+    uint64_t* regions = nullptr;
+    uint32_t* counts = nullptr;
+    uint32_t* err = nullptr;  // device flag, see PassA::err
+    uint64_t region_bytes = 0;
+    uint64_t counts_bytes = 0;
+};
 
 struct BuildTimers {
     hipEvent_t t0, t1, t2;
     bool valid = false;
 };
 
-// Builds into d_words32 (OR-accumulate).  `ws` must be sized by the caller for
-// the Partition strategy (partition_sizing).  Records t0/t1/t2 when timers != NULL.
+// Builds into d_words32 (OR-accumulate).  For the Partition strategy the
+// workspace must hold plan_partition(num_bits, k, kb.n, num_cus).  Records
+// t0/t1/t2 (start / pass A done / end) when timers != NULL.
 hipError_t launch_build(const KeyBatch& kb, uint32_t num_bits, uint32_t k, uint32_t* d_words32,
                         BuildStrategy s, const PartitionWorkspace& ws, int num_cus,
                         hipStream_t st, BuildTimers* timers);

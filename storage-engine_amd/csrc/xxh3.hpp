@@ -7,7 +7,7 @@
 // algorithm, shaped for one-key-per-lane GPU execution:
 //   * the 192-byte default secret is held as 24 little-endian u64 words, so a
 //     secret read at a compile-time offset folds to an immediate;
-//   * 64x64->128 products use v_mul_hi/lo (via __umul64hi) on the device;
+//   * 64x64->128 products are four v_mad_u64_u32 on the device;
 //   * key bytes are read with 8-byte unaligned loads (gfx950 global memory
 //     accepts unaligned dword access), never byte-by-byte except for <4 B keys;
 //   * `xxh3_16` is the fixed-16-byte fast path fed straight from a 16-byte
@@ -66,14 +66,23 @@ LSMB_HD uint32_t ld32(const uint8_t* p) {
     return v;
 }
 
+// 64x64 -> 128.  On the device: four v_mad_u64_u32 (32x32+64 -> 64), the
+// minimum; `a*b` plus `__umul64hi` would issue about twice as many multiplies.
 LSMB_HD H128 mul128(uint64_t a, uint64_t b) {
 #ifdef __HIP_DEVICE_COMPILE__
-    return H128{a * b, __umul64hi(a, b)};
+    const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32);
+    const uint32_t b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
+    const uint64_t p00 = (uint64_t)a0 * b0;
+    const uint64_t t = (uint64_t)a0 * b1 + (p00 >> 32);
+    const uint64_t u = (uint64_t)a1 * b0 + (uint32_t)t;
+    return H128{(u << 32) | (uint32_t)p00, (uint64_t)a1 * b1 + (t >> 32) + (u >> 32)};
 #else
     unsigned __int128 r = (unsigned __int128)a * b;
     return H128{(uint64_t)r, (uint64_t)(r >> 64)};
 #endif
 }
+// High 64 bits of a 64x64 product.
+LSMB_HD uint64_t mulhi64(uint64_t a, uint64_t b) { return mul128(a, b).hi; }
 LSMB_HD uint64_t fold(uint64_t a, uint64_t b) {
     H128 r = mul128(a, b);
     return r.lo ^ r.hi;

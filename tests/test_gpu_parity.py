@@ -98,7 +98,8 @@ def _cmp(a, b):
 
 
 @pytest.mark.parametrize("n,fpr", [(1, 0.01), (1000, 0.01), (70_000, 0.001), (300_000, 0.01),
-                                   (2_000_001, 0.01), (5_000_000, 0.05)])
+                                   (2_000_001, 0.01), (5_000_000, 0.05), (7_000_000, 0.01),
+                                   (12_345_678, 0.001)])
 def test_build_fixed16_vs_oracle(ctx, oracle, n, fpr):
     keys = keygen.key16(0x5EED0001, 0, n)
     nb, k = lsmbloom.params(n, fpr)
@@ -123,12 +124,13 @@ def test_build_few_keys_huge_filter_atomic(ctx, oracle):
 
 
 def test_build_duplicate_heavy_overflow(ctx, oracle):
-    # 2M copies of one key + 1M distinct: a few slices receive far more than
-    # their expected share, exercising the run-overflow path.
-    n = 3_000_000
+    # 2M copies of one key + 8M distinct: the 7 slices of the repeated key get
+    # far more than their expected share, exercising the region-overflow path.
+    n = 10_000_000
     keys = keygen.key16(0xD00D, 0, n)
     keys[: 2_000_000] = keys[0]
     nb, k = lsmbloom.params(n, 0.01)
+    assert lsmbloom.build_strategy(nb, n) == "partition"
     _cmp(ctx.build_fixed(keys, 16, nb, k), oracle.build_fixed_mt(keys, 16, nb, k, 16))
 
 

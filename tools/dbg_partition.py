@@ -1,0 +1,28 @@
+"""Debug sweep of the partition build over (n, num_bits, k): reports errors and timing."""
+import sys
+import time
+
+sys.path.insert(0, "storage-engine_amd")
+import torch  # noqa: E402
+
+import lsmbloom  # noqa: E402
+
+ctx = lsmbloom.Context(0)
+dev = torch.device("cuda:0")
+cfgs = [(int(a), int(b), int(c)) for a, b, c in (x.split(":") for x in sys.argv[1:])]
+N = max(n for n, _, _ in cfgs)  # the key buffer must hold the largest n
+keys = torch.empty((N, 16), dtype=torch.uint8, device=dev)
+ctx.gen_key16_dev(0x5EED0001, 0, N, keys)
+torch.cuda.synchronize()
+for n, nb, k in cfgs:
+    assert n <= N
+    w = torch.zeros(lsmbloom.num_words(nb), dtype=torch.int64, device=dev)
+    t0 = time.time()
+    try:
+        ctx.build_fixed_dev(keys, 16, n, nb, k, w)
+        ctx.sync()
+        st = "ok"
+    except Exception as e:  # noqa: BLE001
+        st = str(e)
+    print("n=%d nb=%d k=%d strategy=%s %.3fs %s" % (n, nb, k, lsmbloom.build_strategy(nb, n), time.time() - t0, st),
+          flush=True)

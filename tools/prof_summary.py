@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Condense a tools/profile.sh output directory into a markdown summary.
+
+Usage: tools/prof_summary.py gpurun_out/prof_<tag> > profiles/<tag>.md
+FETCH_SIZE/WRITE_SIZE are in KiB; FETCH_SIZE is doubled (gfx950 tallies a
+wide coalesced stream's 128-B requests at 64 B: MI355X_MICROARCH.md §HBM).
+"""
+import collections
+import csv
+import os
+import sys
+
+
+def short(name):
+    n = name.replace("lsmb::(anonymous namespace)::", "").replace("lsmb::", "").replace("void ", "")
+    n = n.split("(")[0]
+    return n[:90]
+
+
+def main(d):
+    print("# rocprofv3 summary: %s\n" % os.path.basename(d.rstrip("/")))
+    ks = os.path.join(d, "stats", "run_kernel_stats.csv")
+    if os.path.exists(ks):
+        print("## Kernel time (rocprofv3 --kernel-trace --stats)\n")
+        print("| kernel | calls | avg us | total % |")
+        print("|---|---|---|---|")
+        for r in csv.DictReader(open(ks)):
+            print("| %s | %s | %.2f | %.1f |" % (short(r["Name"]), r["Calls"], float(r["AverageNs"]) / 1e3,
+                                                float(r["Percentage"])))
+        print()
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for sub in ("fetch", "write", "sq1", "sq2"):
+        p = os.path.join(d, sub, "run_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        for r in csv.DictReader(open(p)):
+            agg[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    if agg:
+        print("## PMC counters (mean per dispatch)\n")
+        for kn, cs in sorted(agg.items()):
+            if not any(x in kn for x in ("k_", "lsmb")):
+                continue
+            m = {c: sum(v) / len(v) for c, v in cs.items()}
+            extra = []
+            if "FETCH_SIZE" in m:
+                extra.append("HBM read (FETCH_SIZE x2) = %.1f MB" % (2 * m["FETCH_SIZE"] * 1024 / 1e6))
+            if "WRITE_SIZE" in m:
+                extra.append("HBM write = %.1f MB" % (m["WRITE_SIZE"] * 1024 / 1e6))
+            print("- **%s**: %s" % (kn, ", ".join(extra)))
+            for c in sorted(m):
+                print("  - %s = %.4g" % (c, m[c]))
+        print()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

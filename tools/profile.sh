@@ -1,0 +1,21 @@
+#!/bin/bash
+# rocprofv3 profile of bench.py on one MI355X (run through gpurun).
+# Usage: tools/profile.sh <tag> [extra bench args]
+# Writes gpurun_out/prof_<tag>/{stats,fetch,write,sq1,sq2}/; tools/prof_summary.py condenses them.
+set -euo pipefail
+TAG=${1:-r01}; shift || true
+REPO=${GRAFT_REPO_ROOT:-/root/repo}
+OUT=$REPO/gpurun_out/prof_$TAG
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+BENCH="$REPO/bench.py --steps 10 --warmup 2 --no-cpu-baseline $*"
+run() {  # name, rocprofv3 args...
+  local name=$1; shift
+  timeout -k 10 300 rocprofv3 "$@" --output-format csv -d "$OUT/$name" -o run -- python3 $BENCH > "$OUT/$name.log" 2>&1
+}
+run stats --kernel-trace --stats
+run fetch --pmc FETCH_SIZE
+run write --pmc WRITE_SIZE
+run sq1 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_WAIT_INST_LDS
+run sq2 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_BUSY_CYCLES
+echo "profile $TAG done"
