@@ -1,0 +1,241 @@
+// bloom_tests.cpp — the reference's bloom tests, restated against the C++
+// mirror (storage-engine_amd/cpp/lsm_bloom.hpp).  Each test cites the Rust
+// test it follows (G1DO/Storage-Engine tests/bloom_tests.rs,
+// tests/bloom_serialize_tests.rs, tests/bloom_sstable_integration_tests.rs).
+// Usage: bloom_tests [--gpu]   (--gpu adds the BloomFilterBuilder/batch tests)
+#include <stdio.h>
+#include <string.h>
+
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../../storage-engine_amd/cpp/lsm_bloom.hpp"
+
+using lsm::bloom::BloomFilter;
+using lsm::bloom::BloomFilterBuilder;
+using lsm::bloom::Corruption;
+
+static int g_fail = 0, g_run = 0;
+#define CHECK(c)                                                              \
+    do {                                                                      \
+        if (!(c)) {                                                           \
+            fprintf(stderr, "  FAILED %s:%d: %s\n", __FILE__, __LINE__, #c); \
+            throw 1;                                                          \
+        }                                                                     \
+    } while (0)
+
+template <class E, class F>
+static bool throws(F&& f) {
+    try {
+        f();
+    } catch (const E&) {
+        return true;
+    }
+    return false;
+}
+
+static void run(const char* name, const std::function<void()>& f) {
+    g_run++;
+    try {
+        f();
+        printf("ok   %s\n", name);
+    } catch (...) {
+        g_fail++;
+        printf("FAIL %s\n", name);
+    }
+}
+
+static std::string bin(std::initializer_list<int> b) {
+    std::string s;
+    for (int x : b) s.push_back((char)x);
+    return s;
+}
+
+int main(int argc, char** argv) {
+    const bool gpu = argc > 1 && strcmp(argv[1], "--gpu") == 0;
+
+    // ---- tests/bloom_tests.rs
+    run("empty_filter_returns_false (bloom_tests.rs:4)", [] {
+        BloomFilter bf(100, 0.01);
+        CHECK(!bf.may_contain("any_key") && !bf.may_contain("hello") && !bf.may_contain(""));
+    });
+    run("inserted_key_found (bloom_tests.rs:14)", [] {
+        BloomFilter bf(100, 0.01);
+        bf.insert("hello");
+        CHECK(bf.may_contain("hello"));
+    });
+    run("different_key_not_found (bloom_tests.rs:23)", [] {
+        BloomFilter bf(100, 0.01);
+        bf.insert("hello");
+        CHECK(!bf.may_contain("world") && !bf.may_contain("hello!") && !bf.may_contain("hell"));
+    });
+    run("duplicate_insert_no_error (bloom_tests.rs:37)", [] {
+        BloomFilter bf(100, 0.01);
+        bf.insert("key");
+        bf.insert("key");
+        bf.insert("key");
+        CHECK(bf.may_contain("key"));
+    });
+    run("multiple_keys (bloom_tests.rs:50)", [] {
+        BloomFilter bf(100, 0.01);
+        for (auto k : {"apple", "banana", "cherry"}) bf.insert(k);
+        for (auto k : {"apple", "banana", "cherry"}) CHECK(bf.may_contain(k));
+        CHECK(!bf.may_contain("date") && !bf.may_contain("elderberry"));
+    });
+    run("false_positive_rate (bloom_tests.rs:68)", [] {
+        const int n = 10000;
+        BloomFilter bf(n, 0.01);
+        for (int i = 0; i < n; i++) bf.insert("key_" + std::to_string(i));
+        int fp = 0;
+        for (int i = n; i < 2 * n; i++) fp += bf.may_contain("key_" + std::to_string(i));
+        const double r = fp / (double)n;
+        CHECK(r < 0.02 && (r > 0.001 || fp == 0));
+        CHECK(fp == 90);  // golden: tests/golden/bloom_kats.json "false_positive_rate"
+    });
+    run("various_fpr_values (bloom_tests.rs:113)", [] {
+        const double fprs[] = {0.10, 0.05, 0.01, 0.001};
+        const char* descs[] = {"10%", "5%", "1%", "0.1%"};
+        for (int t = 0; t < 4; t++) {
+            BloomFilter bf(5000, fprs[t]);
+            for (int i = 0; i < 5000; i++) bf.insert(std::string("test_") + descs[t] + "_" + std::to_string(i));
+            int fp = 0;
+            for (int i = 5000; i < 10000; i++)
+                fp += bf.may_contain(std::string("test_") + descs[t] + "_" + std::to_string(i));
+            CHECK(fp / 5000.0 < fprs[t] * 3.0);
+        }
+    });
+    run("empty_key (bloom_tests.rs:151)", [] {
+        BloomFilter bf(100, 0.01);
+        bf.insert("");
+        CHECK(bf.may_contain(""));
+    });
+    run("large_key (bloom_tests.rs:160)", [] {
+        BloomFilter bf(100, 0.01);
+        std::string big(1 << 20, '\0');
+        bf.insert(big);
+        CHECK(bf.may_contain(big));
+    });
+    run("binary_keys (bloom_tests.rs:170)", [] {
+        BloomFilter bf(100, 0.01);
+        const std::string k1 = bin({0x00, 0x01, 0x02, 0xFF, 0xFE}), k2 = bin({0xFF, 0xFE, 0xFD, 0xFC});
+        bf.insert(k1);
+        CHECK(bf.may_contain(k1) && !bf.may_contain(k2));
+    });
+    run("new panics on bad arguments (mod.rs:39-43)", [] {
+        CHECK(throws<std::invalid_argument>([] { BloomFilter(0, 0.01); }));
+        CHECK(throws<std::invalid_argument>([] { BloomFilter(10, 0.0); }));
+        CHECK(throws<std::invalid_argument>([] { BloomFilter(10, 1.0); }));
+    });
+
+    // ---- tests/bloom_serialize_tests.rs
+    run("serialize_deserialize_roundtrip (bloom_serialize_tests.rs:4)", [] {
+        BloomFilter bf(100, 0.01);
+        for (auto k : {"hello", "world", "foo"}) bf.insert(k);
+        BloomFilter bf2 = BloomFilter::deserialize(bf.serialize());
+        for (auto k : {"hello", "world", "foo"}) CHECK(bf2.may_contain(k));
+        CHECK(!bf2.may_contain("bar") && !bf2.may_contain("baz"));
+    });
+    run("serialize_empty_filter (bloom_serialize_tests.rs:28)", [] {
+        BloomFilter bf2 = BloomFilter::deserialize(BloomFilter(100, 0.01).serialize());
+        CHECK(!bf2.may_contain("anything") && !bf2.may_contain(""));
+    });
+    run("serialize_large_filter (bloom_serialize_tests.rs:41)", [] {
+        BloomFilter bf(10000, 0.01);
+        for (int i = 0; i < 10000; i++) bf.insert("key_" + std::to_string(i));
+        BloomFilter bf2 = BloomFilter::deserialize(bf.serialize());
+        for (int i = 0; i < 10000; i++) CHECK(bf2.may_contain("key_" + std::to_string(i)));
+    });
+    run("deserialize_garbage (bloom_serialize_tests.rs:61)", [] {
+        CHECK(throws<Corruption>([] { BloomFilter::deserialize(std::vector<uint8_t>{0xFF, 0xFF, 0xFF, 0xFF}); }));
+        CHECK(throws<Corruption>([] { BloomFilter::deserialize(std::vector<uint8_t>{}); }));
+    });
+    run("deserialize_truncated (bloom_serialize_tests.rs:72)", [] {
+        std::vector<uint8_t> d = {7, 0, 0, 0, 0xE8, 0x03, 0, 0, 100, 0, 0, 0};
+        CHECK(throws<Corruption>([&] { BloomFilter::deserialize(d); }));
+    });
+    run("deserialize_extra_data (bloom_serialize_tests.rs:84)", [] {
+        BloomFilter bf(10, 0.01);
+        bf.insert("test");
+        auto b = bf.serialize();
+        for (char c : std::string("extra")) b.push_back((uint8_t)c);
+        CHECK(throws<Corruption>([&] { BloomFilter::deserialize(b); }));
+    });
+    run("serialized_size (bloom_serialize_tests.rs:95)", [] {
+        BloomFilter bf(1000, 0.01);
+        const size_t words = bf.num_bits() / 64 + (bf.num_bits() % 64 ? 1 : 0);
+        CHECK(bf.serialize().size() == 12 + words * 8);
+    });
+    run("serialize_different_fpr (bloom_serialize_tests.rs:113)", [] {
+        for (double fpr : {0.1, 0.05, 0.01, 0.001}) {
+            BloomFilter bf(1000, fpr);
+            bf.insert("test_key");
+            CHECK(BloomFilter::deserialize(bf.serialize()).may_contain("test_key"));
+        }
+    });
+    run("serialize_binary_keys (bloom_serialize_tests.rs:127)", [] {
+        BloomFilter bf(100, 0.01);
+        const std::string k1 = bin({0x00, 0x01, 0x02, 0xFF}), k2 = bin({0xFF, 0xFE, 0xFD, 0xFC});
+        bf.insert(k1);
+        BloomFilter bf2 = BloomFilter::deserialize(bf.serialize());
+        CHECK(bf2.may_contain(k1) && !bf2.may_contain(k2));
+    });
+    run("serialize_verify_fields_preserved (bloom_serialize_tests.rs:144)", [] {
+        BloomFilter bf(5000, 0.05);
+        BloomFilter bf2 = BloomFilter::deserialize(bf.serialize());
+        CHECK(bf2.num_hashes() == bf.num_hashes() && bf2.num_bits() == bf.num_bits());
+    });
+
+    if (gpu) {
+        // ---- the builder path (SSTableBuilder -> BloomFilterBuilder, src/sstable/builder.rs:74,93,177)
+        run("builder matches single-key inserts (builder.rs:14-28)", [] {
+            BloomFilterBuilder b(1000, 0.01);  // SSTableBuilder::new sizing
+            BloomFilter ref(1000, 0.01);
+            char k[16];
+            for (int i = 0; i < 100; i++) {
+                snprintf(k, sizeof k, "key_%05d", i);
+                b.add_key(k);
+                ref.insert(k);
+            }
+            BloomFilter bf = b.build();
+            CHECK(bf.words() == ref.words());
+            CHECK(bf.serialize() == ref.serialize());
+        });
+        run("sstable bloom: existing found, absent rejected (integration_tests.rs:12-59)", [] {
+            BloomFilterBuilder b(1000, 0.01);
+            char k[16];
+            for (int i = 0; i < 100; i++) {
+                snprintf(k, sizeof k, "key_%05d", i);
+                b.add_key(k);
+            }
+            BloomFilter bf = b.build();
+            for (int i = 0; i < 100; i++) {
+                snprintf(k, sizeof k, "key_%05d", i);
+                CHECK(bf.may_contain(k));
+            }
+        });
+        run("sstable bloom fpr, batched probe (integration_tests.rs:66-113)", [] {
+            BloomFilterBuilder b(1000, 0.01);
+            char k[16];
+            for (int i = 0; i < 1000; i++) {
+                snprintf(k, sizeof k, "exist_%06d", i);
+                b.add_key(k);
+            }
+            BloomFilter bf = b.build();
+            std::vector<std::string> keys;
+            for (int i = 1000; i < 11000; i++) {
+                snprintf(k, sizeof k, "exist_%06d", i);
+                keys.push_back(k);
+            }
+            auto m = BloomFilter::may_contain_batch({&bf}, keys);
+            int fp = 0;
+            for (size_t i = 0; i < keys.size(); i++) {
+                CHECK((m[i] & 1) == bf.may_contain(keys[i]));
+                fp += m[i] & 1;
+            }
+            CHECK(fp == 106);  // golden: bloom_kats.json "sstable_exist_fpr"
+        });
+    }
+    printf("%d/%d passed\n", g_run - g_fail, g_run);
+    return g_fail ? 1 : 0;
+}
