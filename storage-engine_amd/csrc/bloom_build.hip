@@ -195,28 +195,37 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
     uint32_t* claims = slots + (size_t)a.nb * kSegEntries;  // nb
     uint32_t* done = claims + a.nb;                         // nb
     uint32_t* cur = done + a.nb;                            // nb
-    const uint32_t tid = threadIdx.x, w = blockIdx.x;
+    uint32_t* jobs = cur + a.nb;                            // 16 per wave: cooperative flush queue
+    const uint32_t tid = threadIdx.x, w = blockIdx.x, lane = tid & 63;
+    uint32_t* myjobs = jobs + (tid >> 6) * 16;
     for (uint32_t i = tid; i < a.nb * (kSegEntries + 3); i += kBinBlock) smem32[i] = 0;
     __syncthreads();
 
     // Workgroup w owns keys [w*per, (w+1)*per): a contiguous, coalesced run.
     const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
     const uint64_t i0 = (uint64_t)w * per, i1 = min(n, i0 + per);
-    for (uint64_t i = i0 + tid; i < i1; i += kBinBlock) {
-        const H128 h = src.hash(i);
-        W walk(md, h.lo, h.hi);
+    // The loop is uniform across the workgroup (lanes past i1 just carry no
+    // positions): the cooperative flush below needs every lane of the wave.
+    const uint64_t iters = i1 > i0 ? (i1 - i0 + kBinBlock - 1) / kBinBlock : 0;
+    for (uint64_t it = 0; it < iters; it++) {
+        const uint64_t i = i0 + it * kBinBlock + tid;
         uint32_t lb[KMAX], off[KMAX], slot[KMAX], dn[KMAX];
 #pragma unroll
-        for (int q = 0; q < KMAX; q++) {
-            lb[q] = 0xFFFFFFFFu;
-            if ((uint32_t)q < k) {
-                const uint32_t p = walk.pos();
-                const uint32_t b = (p >> kSliceLog2) - a.b0;
-                if (b < a.nb) {
-                    lb[q] = b;
-                    off[q] = p & kSliceMask;
+        for (int q = 0; q < KMAX; q++) lb[q] = 0xFFFFFFFFu;
+        if (i < i1) {
+            const H128 h = src.hash(i);
+            W walk(md, h.lo, h.hi);
+#pragma unroll
+            for (int q = 0; q < KMAX; q++) {
+                if ((uint32_t)q < k) {
+                    const uint32_t p = walk.pos();
+                    const uint32_t b = (p >> kSliceLog2) - a.b0;
+                    if (b < a.nb) {
+                        lb[q] = b;
+                        off[q] = p & kSliceMask;
+                    }
+                    walk.next(md);
                 }
-                walk.next(md);
             }
         }
 #pragma unroll
@@ -241,14 +250,57 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
                     rmask |= 1u << q;
             }
         }
-        while (fmask) {
-            const int qs = __ffs(fmask) - 1;
-            fmask &= fmask - 1;
+        // Wave-cooperative flushes: a store instruction costs the same
+        // whatever its active lanes, so completed segments are written 16 at
+        // a time, 4 lanes x 16 B each, instead of 4 stores by each owner.
+        // Each round the wave's owners (lanes with a completed segment) post
+        // their slice in this wave's LDS job list; lane 4j+p packs piece p of
+        // job j (offsets 6p..6p+5) and stores it; then the owners re-open
+        // their buffers.  All in program order within one wave: no waiting.
+        while (true) {
+            const bool have = fmask != 0;
             uint32_t L = 0;
+            if (have) {
+                const int qs = __ffs(fmask) - 1;
 #pragma unroll
-            for (int q = 0; q < KMAX; q++)
-                if (q == qs) L = lb[q];
-            flush_segment(a, slots, claims, done, cur, L, w);
+                for (int q = 0; q < KMAX; q++)
+                    if (q == qs) L = lb[q];
+            }
+            const uint64_t bal = __ballot(have);
+            if (bal == 0) break;
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+            const bool served = have && rank < 16;
+            if (served) lds_store_volatile(myjobs + rank, L);
+            const uint32_t njobs = min(16u, (uint32_t)__popcll(bal));
+            const uint32_t j = lane >> 2, piece = lane & 3;
+            if (j < njobs) {
+                const uint32_t JL = lds_load_volatile(myjobs + j);
+                const uint32_t c = lds_load_volatile(cur + JL);
+                const uint32_t* sl = slots + JL * kSegEntries + 6 * piece;
+                uint32_t e[6];
+#pragma unroll
+                for (int t = 0; t < 6; t++) e[t] = lds_load_volatile(sl + t);
+                const uint32_t b = a.b0 + JL;
+                if (c < a.cap) {
+                    uint4* dst = reinterpret_cast<uint4*>(region_ptr(a, b, w) + (uint64_t)c * kSegWords) + piece;
+                    *dst = make_uint4(e[0] | (e[1] << 20), (e[1] >> 12) | (e[2] << 8), e[3] | (e[4] << 20),
+                                      (e[4] >> 12) | (e[5] << 8));
+                } else {
+#pragma unroll
+                    for (int t = 0; t < 6; t++) {
+                        const uint32_t p = (b << kSliceLog2) | e[t];
+                        atomicOr(a.gw + (p >> 5), 1u << (p & 31));
+                    }
+                }
+            }
+            if (served) {
+                const uint32_t c = lds_load_volatile(cur + L);
+                lds_store_volatile(cur + L, c + 1);
+                lds_store_volatile(done + L, 0);
+                lds_store_volatile(claims + L, 0);
+                fmask &= fmask - 1;
+            }
         }
         // Retry loop with a WAVE-UNIFORM exit (ballot): every lane's claim,
         // write, done-count and flush happen inside the iteration that makes
@@ -257,7 +309,15 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
         // wave-mates are done: a wave-mate waiting on that very segment then
         // never sees it complete.)
         uint32_t idle = 0;
+#ifdef LSMB_STATS
+        if (rmask) atomicAdd(a.err + 9, (uint32_t)__popc(rmask));          // void claims
+        if (__ballot(rmask != 0) && lane == 0) atomicAdd(a.err + 10, 1u);  // wave-iterations that retry
+        if (lane == 0) atomicAdd(a.err + 11, 1u);                          // wave-iterations
+#endif
         for (uint32_t spin = 0; __ballot(rmask != 0); spin++) {
+#ifdef LSMB_STATS
+            if (lane == 0) atomicAdd(a.err + 12, 1u);  // retry-loop iterations
+#endif
             if (rmask) {
                 const int qs = __ffs(rmask) - 1;
                 uint32_t L = 0, O = 0;
@@ -424,7 +484,7 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
             a.counts = ws.counts;
             a.gw = gw;
             a.err = ws.err;
-            const size_t smem = (size_t)a.nb * kLdsBytesPerBin;
+            const size_t smem = (size_t)a.nb * kLdsBytesPerBin + (kBinBlock / 64) * 16 * 4;
             auto go = [&](auto kern) {
                 hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
                 kern<<<dim3(pl.grid), dim3(kBinBlock), smem, st>>>(src, n, md, k, a);

@@ -125,6 +125,15 @@ hipStream_t pick_stream(lsmb_ctx* c, void* stream) {
 // Reads (and clears) the kernels' device error flag.  Requires the work that
 // could set it to have completed.
 int check_device_error(lsmb_ctx* c) {
+#ifdef LSMB_STATS
+    {
+        uint32_t st[16];
+        HIP_TRY(hipMemcpy(st, c->err.p, 64, hipMemcpyDeviceToHost));
+        fprintf(stderr, "[lsmb stats] void=%u retry_wave_iters=%u wave_iters=%u retry_loop_iters=%u\n", st[9], st[10],
+                st[11], st[12]);
+        HIP_TRY(hipMemset((char*)c->err.p + 36, 0, 28));
+    }
+#endif
     HIP_TRY(hipMemcpy(c->err_host, c->err.p, 32, hipMemcpyDeviceToHost));
     if (*c->err_host) {
         uint32_t e[8];

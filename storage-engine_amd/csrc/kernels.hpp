@@ -18,7 +18,7 @@ constexpr int kBinBlock = 1024;                       // pass A workgroup
 constexpr int kApplyBlock = 1024;                     // pass B workgroup
 constexpr uint32_t kLdsFilterMaxWords32 = 40 * 1024;  // 160 KiB: whole filter in LDS
 constexpr uint32_t kLdsBytesPerBin = kSegEntries * 4 + 12;  // 24 slots + claims/done/cursor
-constexpr uint32_t kMaxBinsPerSweep = 1400;                // 151 KiB of pass A LDS
+constexpr uint32_t kMaxBinsPerSweep = 1380;                // <= 149 KiB of pass A LDS (+ 1 KiB flush queues)
 
 // How a key batch is presented to the kernels.
 struct KeyBatch {

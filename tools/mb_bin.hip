@@ -100,6 +100,18 @@ __global__ __launch_bounds__(BLOCK) void k(const uint4* keys, uint64_t n, Mod32 
                                   v[6 * j + 3] | (v[6 * j + 4] << 20), (v[6 * j + 4] >> 12) | (v[6 * j + 5] << 8));
             if (STAGE == 3) {
                 acc += o[0].x ^ o[1].y ^ o[2].z ^ o[3].w;
+            } else if (STAGE == 5) {  // same stores, regular per-lane addresses
+                uint4* dst = out + ((uint64_t)(blockIdx.x * BLOCK + threadIdx.x) * 64 + (i & 63)) * 4;
+#pragma unroll
+                for (int j = 0; j < 4; j++) dst[j] = o[j];
+            } else if (STAGE == 6) {  // scattered, nontemporal
+                uint4* dst = out + ((uint64_t)(L * gridDim.x + blockIdx.x) * 64 + (i & 63)) * 4;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    typedef unsigned int v4 __attribute__((ext_vector_type(4)));
+                    v4 x = {o[j].x, o[j].y, o[j].z, o[j].w};
+                    __builtin_nontemporal_store(x, reinterpret_cast<v4*>(dst + j));
+                }
             } else {
                 uint4* dst = out + ((uint64_t)(L * gridDim.x + blockIdx.x) * 64 + (i & 63)) * 4;
 #pragma unroll
@@ -143,5 +155,7 @@ int main() {
     run(k<2, 1024>, 1024, 1, "stage 2 + slot writes + done adds");
     run(k<3, 1024>, 1024, 1, "stage 3 + flush reads/pack");
     run(k<4, 1024>, 1024, 1, "stage 4 + global segment stores");
+    run(k<5, 1024>, 1024, 1, "stage 5 = 4 with per-lane regular addresses");
+    run(k<6, 1024>, 1024, 1, "stage 6 = 4 with nontemporal stores");
     return 0;
 }
