@@ -42,7 +42,7 @@ extern "C" {
 #define LSMB_ECORRUPT (-4) /* serialized filter fails validation               */
 #define LSMB_ENOMEM (-5)   /* device or pinned-host allocation failed          */
 
-#define LSMB_ABI_VERSION 1
+#define LSMB_ABI_VERSION 2
 
 typedef struct lsmb_ctx lsmb_ctx; /* one GPU: stream, events, scratch arenas */
 
@@ -153,6 +153,49 @@ int lsmb_or_reduce_dev(lsmb_ctx* ctx, void* d_dst, const void* d_src, uint64_t n
  * for i in [first, first+n). */
 int lsmb_gen_key16_dev(lsmb_ctx* ctx, uint64_t seed, uint64_t first, uint64_t n, void* d_keys,
                        void* stream);
+
+/* ---- device-resident filter sets (multi-get pre-check) --------------------- */
+/* An lsmb_fset keeps up to 64 SSTable filters resident in device memory, each
+ * with its table's key range [min_key, max_key] (SSTable meta,
+ * src/sstable/reader.rs:192).  A probe answers, per key and per filter, the two
+ * checks SSTable::get makes before it touches the index (reader.rs:192-199):
+ *     min_key <= key <= max_key   (byte-wise lexicographic, as Rust's [u8] Ord)
+ *     && may_contain(filter, key)
+ * for a whole batch of keys, so DB::get (src/db/mod.rs:243-267), which today
+ * re-opens and re-deserializes every SSTable per lookup (mod.rs:245,259), can
+ * keep its filters on the GPU and read only the tables a key may be in.
+ * A set belongs to one context and is used from one thread at a time. */
+typedef struct lsmb_fset lsmb_fset;
+
+int lsmb_fset_open(lsmb_ctx* ctx, lsmb_fset** out);
+void lsmb_fset_close(lsmb_fset* fs);
+
+/* Adds a filter from its serialized bloom block (the bytes BloomFilter::serialize
+ * wrote, src/bloom/mod.rs:102-115), validated exactly as BloomFilter::deserialize
+ * (mod.rs:123-168; LSMB_ECORRUPT) and copied straight into device memory.
+ * Returns the filter's slot (0..63, bit `slot` of the probe mask) or < 0. */
+int lsmb_fset_add(lsmb_fset* fs, const uint8_t* block, uint64_t len, const uint8_t* min_key,
+                  uint64_t min_len, const uint8_t* max_key, uint64_t max_len);
+
+/* Same from in-memory filter words (ceil(num_bits/64) LE u64). */
+int lsmb_fset_add_words(lsmb_fset* fs, const uint64_t* words, uint32_t num_bits, uint32_t num_hashes,
+                        const uint8_t* min_key, uint64_t min_len, const uint8_t* max_key,
+                        uint64_t max_len);
+
+/* Drops a filter (e.g. its table was compacted away); the slot is re-used. */
+int lsmb_fset_remove(lsmb_fset* fs, int slot);
+
+/* Bit s set = slot s holds a filter. */
+uint64_t lsmb_fset_live_mask(const lsmb_fset* fs);
+
+/* out_mask[i] bit s = (min_s <= key i <= max_s) && may_contain(filter s, key i).
+ * offsets == NULL selects fixed-length keys of key_len bytes.  Synchronous. */
+int lsmb_fset_probe(lsmb_fset* fs, const uint8_t* data, const uint64_t* offsets, uint32_t key_len,
+                    uint64_t n, uint64_t* out_mask);
+
+/* Device-memory keys and output (u64 per key); asynchronous on `stream`. */
+int lsmb_fset_probe_dev(lsmb_fset* fs, const void* d_data, const void* d_offsets, uint32_t key_len,
+                        uint64_t n, void* d_out_mask, void* stream);
 
 /* ---- introspection ------------------------------------------------------- */
 

@@ -169,4 +169,43 @@ class BloomFilterBuilder {
     std::vector<uint64_t> offsets_;
 };
 
+// Device-resident SSTable filters with key ranges (lsmb_fset): probe(keys)[i]
+// bit s = (min_s <= key i <= max_s) && may_contain(filter s, key i), the
+// checks SSTable::get makes before reading the index (reader.rs:192-199).
+class FilterSet {
+   public:
+    explicit FilterSet(Context& ctx = Context::shared()) { check(lsmb_fset_open(ctx.get(), &fs_)); }
+    ~FilterSet() { lsmb_fset_close(fs_); }
+    FilterSet(const FilterSet&) = delete;
+    FilterSet& operator=(const FilterSet&) = delete;
+
+    // From a serialized bloom block (throws Corruption like deserialize); returns the slot.
+    int add(const std::vector<uint8_t>& block, std::string_view min_key, std::string_view max_key) {
+        return check(lsmb_fset_add(fs_, block.data(), block.size(), u8(min_key), min_key.size(), u8(max_key),
+                                   max_key.size()));
+    }
+    int add(const BloomFilter& f, std::string_view min_key, std::string_view max_key) {
+        return check(lsmb_fset_add_words(fs_, f.words().data(), f.num_bits(), f.num_hashes(), u8(min_key),
+                                         min_key.size(), u8(max_key), max_key.size()));
+    }
+    void remove(int slot) { check(lsmb_fset_remove(fs_, slot)); }
+    uint64_t live_mask() const { return lsmb_fset_live_mask(fs_); }
+
+    std::vector<uint64_t> probe(const std::vector<std::string>& keys) {
+        std::vector<uint64_t> offs(keys.size() + 1, 0);
+        std::string data;
+        for (size_t i = 0; i < keys.size(); i++) {
+            data += keys[i];
+            offs[i + 1] = data.size();
+        }
+        std::vector<uint64_t> out(keys.size());
+        check(lsmb_fset_probe(fs_, u8(data), offs.data(), 0, keys.size(), out.data()));
+        return out;
+    }
+
+   private:
+    static const uint8_t* u8(std::string_view s) { return reinterpret_cast<const uint8_t*>(s.data()); }
+    lsmb_fset* fs_ = nullptr;
+};
+
 }  // namespace lsm::bloom

@@ -87,28 +87,8 @@ struct PassA {
     uint64_t* regions;      // [nbins][grid][cap][8] u64
     uint32_t* counts;       // [nbins][grid] segments written
     uint32_t* gw;           // filter words (overflow fallback only)
-    uint32_t* err;          // set to 1 if a bounded wait ever times out (a bug; never expected)
+    uint32_t* err;          // device error word: nonzero = a waiting loop hit LSMB_SPIN_LIMIT (a bug)
 };
-
-// Every wait in pass A is bounded: a protocol bug must surface as an error
-// (LSMB_EHIP at the next sync), never as a hung GPU.
-#ifndef LSMB_SPIN_LIMIT
-#define LSMB_SPIN_LIMIT (1u << 22)
-#endif
-constexpr uint32_t kSpinLimit = LSMB_SPIN_LIMIT;
-
-// Exponential backoff for every wait in pass A: pollers must not crowd the
-// LDS that the lanes they wait for need (64 * 2^j clocks, j <= 5).
-__device__ __forceinline__ void backoff(uint32_t spin) {
-    switch (spin < 5 ? spin : 5) {
-        case 0: __builtin_amdgcn_s_sleep(1); break;
-        case 1: __builtin_amdgcn_s_sleep(2); break;
-        case 2: __builtin_amdgcn_s_sleep(4); break;
-        case 3: __builtin_amdgcn_s_sleep(8); break;
-        case 4: __builtin_amdgcn_s_sleep(16); break;
-        default: __builtin_amdgcn_s_sleep(32); break;
-    }
-}
 
 __device__ __forceinline__ uint64_t* region_ptr(const PassA& a, uint32_t b, uint32_t w) {
     return a.regions + ((uint64_t)b * a.grid + w) * a.cap * kSegWords;
@@ -116,102 +96,195 @@ __device__ __forceinline__ uint64_t* region_ptr(const PassA& a, uint32_t b, uint
 
 // LDS accessors through address_space(3) pointers, so every access in the
 // protocol is a DS instruction (a wave's DS operations execute in issue
-// order); a plain generic pointer would compile to FLAT accesses, which are
-// slower and complete out of order.
+// order); a plain generic pointer would compile to FLAT accesses.
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
 typedef __attribute__((address_space(3))) u32x4 lds_v4;
 
-__device__ __forceinline__ lds_u32* to_lds(uint32_t* p) { return (lds_u32*)p; }
-__device__ __forceinline__ uint32_t lds_load_volatile(const uint32_t* p) { return *(volatile lds_u32*)(lds_u32*)(p); }
-__device__ __forceinline__ void lds_store_volatile(uint32_t* p, uint32_t v) { *(volatile lds_u32*)to_lds(p) = v; }
+// Orders this wave's earlier LDS writes before its later LDS atomics as seen
+// by other waves (s_waitcnt lgkmcnt(0)); also a compiler barrier.
+__device__ __forceinline__ void lds_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); }
+__device__ __forceinline__ void lds_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup"); }
 
-// Packs 24 offsets into 8 words (3 x 20 bits each) and writes them as
-// segment `seg` of region (b, w); past the region's capacity (adversarial
-// inputs, e.g. one key repeated millions of times) the offsets go straight
-// into the filter with global atomics instead: exact.  `slot(e)` returns
-// offset e.
-template <class SlotFn>
-__device__ __forceinline__ void write_segment(const PassA& a, SlotFn slot, uint32_t b, uint32_t w, uint32_t seg) {
-    if (seg < a.cap) {
-        uint4* dst = reinterpret_cast<uint4*>(region_ptr(a, b, w) + (uint64_t)seg * kSegWords);
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint64_t w0 = (uint64_t)(slot(6 * j) & kSliceMask) | ((uint64_t)(slot(6 * j + 1) & kSliceMask) << 20) |
-                                ((uint64_t)(slot(6 * j + 2) & kSliceMask) << 40);
-            const uint64_t w1 = (uint64_t)(slot(6 * j + 3) & kSliceMask) |
-                                ((uint64_t)(slot(6 * j + 4) & kSliceMask) << 20) |
-                                ((uint64_t)(slot(6 * j + 5) & kSliceMask) << 40);
-            dst[j] = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
-        }
-    } else {
-        for (int e = 0; e < kSegEntries; e++) {
-            const uint32_t p = (b << kSliceLog2) | (slot(e) & kSliceMask);
-            atomicOr(a.gw + (p >> 5), 1u << (p & 31));
-        }
-    }
+__device__ __forceinline__ void or_pos_global(uint32_t* gw, uint32_t b, uint32_t off) {
+    const uint32_t p = (b << kSliceLog2) | off;
+    atomicOr(gw + (p >> 5), 1u << (p & 31));
 }
 
-// LDS state of pass A, per slice of the sweep:
-//   slots[lb][24]  u32 20-bit offsets of the open segment
-//   claims[lb]     slots handed out (>= 24: segment full, claim void)
-//   done[lb]       slots written
-//   cur[lb]        segments this workgroup has written for the slice
-// A lane claims a slot (ds_add_rtn on claims), writes its offset (ds_write),
-// then counts itself in done (ds_add_rtn).  A wave's DS operations execute in
-// issue order, so the lane whose done-increment returns 23 knows all 24
-// offsets are in place: it flushes the segment and re-opens the buffer
-// (done = 0, then claims = 0).  The claim -> write -> done sequence of every
-// valid claim never waits on anything, so re-opens always happen; the only
-// waiting lanes are void claims (buffer full) polling for the re-open.  That
-// matters under SIMT lockstep: a wave's lanes cannot pass a divergent spin
-// loop until all of them can, so no lane may spin on work another lane could
-// be holding back.  Every wait is bounded (err flag) and backs off.
-__device__ __forceinline__ void flush_segment(const PassA& a, uint32_t* slots, uint32_t* claims, uint32_t* done,
-                                              uint32_t* cur, uint32_t lb, uint32_t w) {
-    const volatile lds_v4* sl4 = (const volatile lds_v4*)to_lds(slots + lb * kSegEntries);  // 16-B aligned
-    uint32_t v[kSegEntries];
-#pragma unroll
-    for (int j = 0; j < kSegEntries / 4; j++) {
-        const u32x4 x = sl4[j];
-        v[4 * j] = x.x;
-        v[4 * j + 1] = x.y;
-        v[4 * j + 2] = x.z;
-        v[4 * j + 3] = x.w;
-    }
-    const uint32_t c = lds_load_volatile(cur + lb);
-    write_segment(a, [&](int e) { return v[e]; }, a.b0 + lb, w, c);
-    lds_store_volatile(cur + lb, c + 1);
-    lds_store_volatile(done + lb, 0);
-    lds_store_volatile(claims + lb, 0);
+// Writes one packed segment (8 words, 24 offsets) as segment `seg` of region (b, w).
+__device__ __forceinline__ void write_segment(const PassA& a, const uint64_t* words, uint32_t b, uint32_t w,
+                                              uint32_t seg) {
+    uint64_t* dst = region_ptr(a, b, w) + (uint64_t)seg * kSegWords;
+    for (int j = 0; j < kSegWords; j++) dst[j] = words[j];
 }
+
+// Pass A LDS state, per slice of the sweep (136 B):
+//   half[lb][2][8]  u64  a ring of two 24-offset segments; entry e of a
+//                        segment is bits [20*(e>>3), +20) of word e&7
+//   state[lb]       u32  [gen1:8 | gen0:8 | claims:16]
+//   done[lb]        u32  [done1:16 | done0:16]
+// plus a 64-entry flush queue per wave.
+// Claim c (0, 1, 2, ...) is entry c%24 of segment s = c/24, which lives in
+// half s&1 and is written as segment s of the workgroup's region; gen_h counts
+// the segments half h has flushed, so the half is free for s exactly when
+// gen_{s&1} == s/2.  A lane claims with ONE ds_add_rtn on state, whose return
+// value is an atomic snapshot of (claims, gen0, gen1):
+//   - half free: OR the offset into it, then count it in done_h (the lane that
+//     brings done_h to 24 queues the segment's flush);
+//   - half still holding segment s-2 (rare): the lane keeps the claim in a
+//     small per-lane deferred list and completes it (OR + done) in a later
+//     iteration, once gen_h shows the half flushed;
+//   - region full (c >= cap*24; adversarial inputs): the claim is undone (the
+//     counter stays bounded) and the bit is set with a global atomic (exact:
+//     pass B reads the filter words after pass A).
+// Queued flushes run at the end of each key iteration, wave-cooperatively;
+// meanwhile the other half takes the slice's new claims.
+// Progress: an immediate claim's OR and done-count follow its claim within
+// the same iteration with no waiting; a deferred claim for segment s waits
+// only for segment s-2's flush, whose claims are immediate or deferred on
+// s-4, and so on down to a segment with only immediate claims.  Every loop
+// that waits (deferred list full, final drain) retries the wave's deferred
+// claims AND flushes its queue on each pass, and exits wave-uniformly
+// (ballot), so no lane ever holds back the work another lane waits for.
+// cap <= kMaxRegionSegs keeps claims < 2^16 and gens < 2^8.
+constexpr int kDefer = 2;       // deferred claims a lane can hold across iterations
+constexpr uint32_t kQueue = 64;  // per-wave flush queue entries
+
+struct BinLds {
+    uint64_t* half;
+    uint32_t* state;
+    uint32_t* done;
+    uint32_t* jq;  // this wave's flush queue: slice*2 + half
+};
+
+// Entry c of its slice: (word index within the slice's 16-word ring, bit shift).
+__device__ __forceinline__ void entry_slot(uint32_t c, uint32_t& word, uint32_t& sh) {
+    const uint32_t sg = c / (uint32_t)kSegEntries, e = c - sg * (uint32_t)kSegEntries;
+    word = ((sg & 1) << 3) | (e & 7);
+    sh = (e >> 3) * 20;
+}
+
+// Flushes the wave's queued segments, 16 per round: lane 4j+p copies piece p
+// (16 B) of job j to the region and zeroes it; then lane j releases job j's
+// half (done_h -= 24, gen_h += 1).  A store instruction costs the same
+// whatever its active lanes, hence the cooperation.
+__device__ __forceinline__ void flush_queue(const PassA& a, const BinLds& L, uint32_t w, uint32_t lane, uint32_t& qn) {
+    for (uint32_t r = 0; r < qn; r += 16) {
+        const uint32_t nj = min(16u, qn - r);
+        const uint32_t j = lane >> 2, piece = lane & 3;
+        if (j < nj) {
+            const uint32_t JJ = *(volatile lds_u32*)(lds_u32*)(L.jq + r + j);
+            const uint32_t JL = JJ >> 1, JH = JJ & 1;
+            const uint32_t g = (*(volatile lds_u32*)(lds_u32*)(L.state + JL) >> (16 + 8 * JH)) & 0xFFu;
+            const uint32_t sg = 2 * g + JH;  // < cap: claims past the region's capacity are undone
+            volatile lds_v4* hp = (volatile lds_v4*)(lds_u64*)(L.half + JL * 16 + JH * 8 + 2 * piece);
+            const u32x4 v = *hp;
+            *hp = u32x4{0, 0, 0, 0};
+            uint4* dst = reinterpret_cast<uint4*>(region_ptr(a, a.b0 + JL, w) + (uint64_t)sg * kSegWords) + piece;
+            *dst = make_uint4(v.x, v.y, v.z, v.w);
+        }
+        lds_release();
+        if (lane < nj) {
+            const uint32_t JJ = *(volatile lds_u32*)(lds_u32*)(L.jq + r + lane);
+            const uint32_t S = JJ >> 1, H = JJ & 1;
+            atomicSub(L.done + S, (uint32_t)kSegEntries << (16 * H));
+            lds_release();
+            atomicAdd(L.state + S, 1u << (16 + 8 * H));
+        }
+#ifdef LSMB_STATS
+        if (lane == 0) atomicAdd(a.err + 12, 1u);
+#endif
+    }
+    qn = 0;
+}
+
+// Appends the lanes' jobs (has) to the wave's queue (flushing first if full).
+__device__ __forceinline__ void queue_job(const PassA& a, const BinLds& L, uint32_t w, uint32_t lane, uint32_t& qn,
+                                          bool has, uint32_t J) {
+    const uint64_t bal = __ballot(has);
+    if (bal == 0) return;
+    const uint32_t cnt = (uint32_t)__popcll(bal);
+    if (qn + cnt > kQueue) flush_queue(a, L, w, lane, qn);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+    if (has) *(volatile lds_u32*)(lds_u32*)(L.jq + qn + rank) = J;
+    qn += cnt;
+}
+
+// Completes the lane's deferred claims whose half has been flushed since and
+// queues the flushes they trigger.
+__device__ __forceinline__ void retry_deferred(const PassA& a, const BinLds& L, uint32_t w, uint32_t lane, uint32_t& qn,
+                                               const uint32_t (&dkey)[kDefer], const uint32_t (&doff)[kDefer],
+                                               uint32_t& dmask) {
+    uint32_t ready = 0;
+    if (dmask) {
+#pragma unroll
+        for (int d = 0; d < kDefer; d++) {
+            if (dmask >> d & 1) {
+                const uint32_t lb = dkey[d] >> 16, c = dkey[d] & 0xFFFFu;
+                const uint32_t sg = c / (uint32_t)kSegEntries, hh = sg & 1;
+                const uint32_t g = (*(volatile lds_u32*)(lds_u32*)(L.state + lb) >> (16 + 8 * hh)) & 0xFFu;
+                if (g == ((sg >> 1) & 0xFFu)) {
+                    uint32_t word, sh;
+                    entry_slot(c, word, sh);
+                    atomicOr(L.half + lb * 16 + word, (uint64_t)doff[d] << sh);
+                    ready |= 1u << d;
+                }
+            }
+        }
+    }
+    if (!__ballot(ready != 0)) return;
+    lds_release();
+    uint32_t dn[kDefer];
+#pragma unroll
+    for (int d = 0; d < kDefer; d++)
+        if (ready >> d & 1)
+            dn[d] = atomicAdd(L.done + (dkey[d] >> 16), 1u << (16 * (((dkey[d] & 0xFFFFu) / (uint32_t)kSegEntries) & 1)));
+    lds_acquire();
+#pragma unroll
+    for (int d = 0; d < kDefer; d++) {
+        const uint32_t hh = ((dkey[d] & 0xFFFFu) / (uint32_t)kSegEntries) & 1;
+        const bool job = (ready >> d & 1) && ((dn[d] >> (16 * hh)) & 0xFFFFu) == (uint32_t)kSegEntries - 1;
+        queue_job(a, L, w, lane, qn, job, (dkey[d] >> 16) * 2 + hh);
+    }
+    dmask &= ~ready;
+}
+
+// Passes a waiting loop may make before pass A reports an internal error
+// (LSMB_EHIP) instead of hanging: never reached unless the protocol is broken.
+#ifndef LSMB_SPIN_LIMIT
+#define LSMB_SPIN_LIMIT (1u << 24)
+#endif
 
 // Pass A.  One key per lane per iteration; W = Walk32 when num_bits <= 2^31,
-// else Walk64.  KMAX bounds k: a key's k claims, writes and done-counts are
-// each issued back to back.
+// else Walk64.  KMAX bounds k.
 template <class Src, class W, int KMAX>
 __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md, uint32_t k, PassA a) {
-    extern __shared__ uint32_t smem32[];
-    uint32_t* slots = smem32;                               // nb * 24
-    uint32_t* claims = slots + (size_t)a.nb * kSegEntries;  // nb
-    uint32_t* done = claims + a.nb;                         // nb
-    uint32_t* cur = done + a.nb;                            // nb
-    uint32_t* jobs = cur + a.nb;                            // 16 per wave: cooperative flush queue
+    extern __shared__ uint64_t smem64[];
+    BinLds L;
+    L.half = smem64;                                    // nb * 16
+    L.state = (uint32_t*)(L.half + (size_t)a.nb * 16);  // nb
+    L.done = L.state + a.nb;                            // nb
     const uint32_t tid = threadIdx.x, w = blockIdx.x, lane = tid & 63;
-    uint32_t* myjobs = jobs + (tid >> 6) * 16;
-    for (uint32_t i = tid; i < a.nb * (kSegEntries + 3); i += kBinBlock) smem32[i] = 0;
+    L.jq = L.done + a.nb + (tid >> 6) * kQueue;
+    const uint32_t climit = a.cap * (uint32_t)kSegEntries;
+    {
+        uint32_t* z = reinterpret_cast<uint32_t*>(smem64);
+        for (uint32_t i = tid; i < a.nb * (kLdsBytesPerBin / 4); i += kBinBlock) z[i] = 0;
+    }
     __syncthreads();
 
+    uint32_t qn = 0;                                 // wave-uniform: queued flushes
+    uint32_t dkey[kDefer], doff[kDefer], dmask = 0;  // deferred claims: (slice << 16 | claim), offset
     // Workgroup w owns keys [w*per, (w+1)*per): a contiguous, coalesced run.
     const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
     const uint64_t i0 = (uint64_t)w * per, i1 = min(n, i0 + per);
     // The loop is uniform across the workgroup (lanes past i1 just carry no
-    // positions): the cooperative flush below needs every lane of the wave.
+    // positions): the cooperative flush needs every lane of the wave.
     const uint64_t iters = i1 > i0 ? (i1 - i0 + kBinBlock - 1) / kBinBlock : 0;
     for (uint64_t it = 0; it < iters; it++) {
         const uint64_t i = i0 + it * kBinBlock + tid;
-        uint32_t lb[KMAX], off[KMAX], slot[KMAX], dn[KMAX];
-#pragma unroll
-        for (int q = 0; q < KMAX; q++) lb[q] = 0xFFFFFFFFu;
+        uint32_t lb[KMAX], off[KMAX], st[KMAX];
+        uint32_t pend = 0;
         if (i < i1) {
             const H128 h = src.hash(i);
             W walk(md, h.lo, h.hi);
@@ -220,152 +293,121 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
                 if ((uint32_t)q < k) {
                     const uint32_t p = walk.pos();
                     const uint32_t b = (p >> kSliceLog2) - a.b0;
-                    if (b < a.nb) {
-                        lb[q] = b;
-                        off[q] = p & kSliceMask;
-                    }
+                    lb[q] = b;
+                    off[q] = p & kSliceMask;
+                    if (b < a.nb) pend |= 1u << q;
                     walk.next(md);
                 }
             }
         }
+        // Claims, issued back to back (a result used inside its own `if`
+        // makes the compiler wait for each in turn).
 #pragma unroll
         for (int q = 0; q < KMAX; q++)
-            if (lb[q] != 0xFFFFFFFFu) slot[q] = atomicAdd(&claims[lb[q]], 1u);
-#pragma unroll
-        for (int q = 0; q < KMAX; q++)
-            if (lb[q] != 0xFFFFFFFFu && slot[q] < (uint32_t)kSegEntries)
-                lds_store_volatile(slots + lb[q] * kSegEntries + slot[q], off[q]);
-#pragma unroll
-        for (int q = 0; q < KMAX; q++)
-            if (lb[q] != 0xFFFFFFFFu && slot[q] < (uint32_t)kSegEntries) dn[q] = atomicAdd(&done[lb[q]], 1u);
-        // flushes (wait-free), then retries of void claims: one code path
-        // each, the operands picked out of the unrolled arrays with selects
-        uint32_t fmask = 0, rmask = 0;
+            if (pend >> q & 1) st[q] = atomicAdd(L.state + lb[q], 1u);
+        // Immediate claims: OR the offset in.  Others: region full -> undo +
+        // global atomic; half busy -> deferred.
+        uint32_t cmask = 0, dnew = 0;
 #pragma unroll
         for (int q = 0; q < KMAX; q++) {
-            if (lb[q] != 0xFFFFFFFFu) {
-                if (slot[q] < (uint32_t)kSegEntries)
-                    fmask |= (uint32_t)(dn[q] == (uint32_t)kSegEntries - 1) << q;
-                else
-                    rmask |= 1u << q;
-            }
-        }
-        // Wave-cooperative flushes: a store instruction costs the same
-        // whatever its active lanes, so completed segments are written 16 at
-        // a time, 4 lanes x 16 B each, instead of 4 stores by each owner.
-        // Each round the wave's owners (lanes with a completed segment) post
-        // their slice in this wave's LDS job list; lane 4j+p packs piece p of
-        // job j (offsets 6p..6p+5) and stores it; then the owners re-open
-        // their buffers.  All in program order within one wave: no waiting.
-        while (true) {
-            const bool have = fmask != 0;
-            uint32_t L = 0;
-            if (have) {
-                const int qs = __ffs(fmask) - 1;
-#pragma unroll
-                for (int q = 0; q < KMAX; q++)
-                    if (q == qs) L = lb[q];
-            }
-            const uint64_t bal = __ballot(have);
-            if (bal == 0) break;
-            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-            const bool served = have && rank < 16;
-            if (served) lds_store_volatile(myjobs + rank, L);
-            const uint32_t njobs = min(16u, (uint32_t)__popcll(bal));
-            const uint32_t j = lane >> 2, piece = lane & 3;
-            if (j < njobs) {
-                const uint32_t JL = lds_load_volatile(myjobs + j);
-                const uint32_t c = lds_load_volatile(cur + JL);
-                const uint32_t* sl = slots + JL * kSegEntries + 6 * piece;
-                uint32_t e[6];
-#pragma unroll
-                for (int t = 0; t < 6; t++) e[t] = lds_load_volatile(sl + t);
-                const uint32_t b = a.b0 + JL;
-                if (c < a.cap) {
-                    uint4* dst = reinterpret_cast<uint4*>(region_ptr(a, b, w) + (uint64_t)c * kSegWords) + piece;
-                    *dst = make_uint4(e[0] | (e[1] << 20), (e[1] >> 12) | (e[2] << 8), e[3] | (e[4] << 20),
-                                      (e[4] >> 12) | (e[5] << 8));
+            if (pend >> q & 1) {
+                const uint32_t c = st[q] & 0xFFFFu, sg = c / (uint32_t)kSegEntries, hh = sg & 1;
+                const uint32_t e = c - sg * (uint32_t)kSegEntries;
+                const bool free_half = ((st[q] >> (16 + 8 * hh)) & 0xFFu) == ((sg >> 1) & 0xFFu);
+                if (c >= climit) {
+                    atomicSub(L.state + lb[q], 1u);
+                    or_pos_global(a.gw, a.b0 + lb[q], off[q]);
+                } else if (free_half) {
+                    atomicOr(L.half + lb[q] * 16 + (hh << 3) + (e & 7), (uint64_t)off[q] << ((e >> 3) * 20));
+                    cmask |= 1u << q;
+                    st[q] = hh;  // from here on: the half
                 } else {
-#pragma unroll
-                    for (int t = 0; t < 6; t++) {
-                        const uint32_t p = (b << kSliceLog2) | e[t];
-                        atomicOr(a.gw + (p >> 5), 1u << (p & 31));
-                    }
+                    dnew |= 1u << q;
                 }
-            }
-            if (served) {
-                const uint32_t c = lds_load_volatile(cur + L);
-                lds_store_volatile(cur + L, c + 1);
-                lds_store_volatile(done + L, 0);
-                lds_store_volatile(claims + L, 0);
-                fmask &= fmask - 1;
             }
         }
-        // Retry loop with a WAVE-UNIFORM exit (ballot): every lane's claim,
-        // write, done-count and flush happen inside the iteration that makes
-        // them.  (With a per-lane `break`, the compiler moves the success
-        // path to the loop exit, which a lane only reaches once all its
-        // wave-mates are done: a wave-mate waiting on that very segment then
-        // never sees it complete.)
-        uint32_t idle = 0;
-#ifdef LSMB_STATS
-        if (rmask) atomicAdd(a.err + 9, (uint32_t)__popc(rmask));          // void claims
-        if (__ballot(rmask != 0) && lane == 0) atomicAdd(a.err + 10, 1u);  // wave-iterations that retry
-        if (lane == 0) atomicAdd(a.err + 11, 1u);                          // wave-iterations
-#endif
-        for (uint32_t spin = 0; __ballot(rmask != 0); spin++) {
-#ifdef LSMB_STATS
-            if (lane == 0) atomicAdd(a.err + 12, 1u);  // retry-loop iterations
-#endif
-            if (rmask) {
-                const int qs = __ffs(rmask) - 1;
-                uint32_t L = 0, O = 0;
+        lds_release();
+        uint32_t dn[KMAX];
 #pragma unroll
-                for (int q = 0; q < KMAX; q++)
-                    if (q == qs) {
-                        L = lb[q];
-                        O = off[q];
-                    }
-                if (lds_load_volatile(claims + L) < (uint32_t)kSegEntries) {  // poll before claiming
-                    const uint32_t s1 = atomicAdd(&claims[L], 1u);
-                    if (s1 < (uint32_t)kSegEntries) {
-                        lds_store_volatile(slots + L * kSegEntries + s1, O);
-                        if (atomicAdd(&done[L], 1u) == (uint32_t)kSegEntries - 1)
-                            flush_segment(a, slots, claims, done, cur, L, w);
-                        rmask &= rmask - 1;
+        for (int q = 0; q < KMAX; q++)
+            if (cmask >> q & 1) dn[q] = atomicAdd(L.done + lb[q], 1u << (16 * st[q]));
+        lds_acquire();
+#ifdef LSMB_STATS
+        if (dnew) atomicAdd(a.err + 9, (uint32_t)__popc(dnew));
+        if (lane == 0) atomicAdd(a.err + 11, 1u);
+#endif
+#pragma unroll
+        for (int q = 0; q < KMAX; q++) {
+            if ((uint32_t)q < k) {
+                const bool job = (cmask >> q & 1) && ((dn[q] >> (16 * st[q])) & 0xFFFFu) == (uint32_t)kSegEntries - 1;
+                queue_job(a, L, w, lane, qn, job, lb[q] * 2 + st[q]);
+            }
+        }
+        // Older deferred claims (their halves may have been flushed since),
+        // then every queued flush.
+        retry_deferred(a, L, w, lane, qn, dkey, doff, dmask);
+        flush_queue(a, L, w, lane, qn);
+        // New deferred claims go to free list entries; while a lane has more
+        // than fit, the wave keeps completing deferred claims and flushing.
+        if (__ballot(dnew != 0)) {
+            for (uint32_t spin = 0;; spin++) {
+#pragma unroll
+                for (int q = 0; q < KMAX; q++) {
+                    if (dnew >> q & 1) {
+                        const int fr = __ffs(~dmask & ((1u << kDefer) - 1)) - 1;
+                        if (fr >= 0) {
+                            const uint32_t c = st[q] & 0xFFFFu;
+#pragma unroll
+                            for (int d = 0; d < kDefer; d++)
+                                if (d == fr) {
+                                    dkey[d] = (lb[q] << 16) | c;
+                                    doff[d] = off[q];
+                                }
+                            dmask |= 1u << fr;
+                            dnew &= ~(1u << q);
+                        }
                     }
                 }
-            }
-            if (spin == kSpinLimit) {
-                if (rmask && atomicOr(a.err, 2u) == 0u) {  // first timeout: dump the stuck slice
-                    const int qs = __ffs(rmask) - 1;
-                    uint32_t L = 0;
-#pragma unroll
-                    for (int q = 0; q < KMAX; q++)
-                        if (q == qs) L = lb[q];
-                    a.err[1] = lds_load_volatile(claims + L);
-                    a.err[2] = lds_load_volatile(done + L);
-                    a.err[3] = lds_load_volatile(cur + L);
-                    a.err[4] = L;
+                if (!__ballot(dnew != 0)) break;
+                if (spin == LSMB_SPIN_LIMIT) {
+                    if (lane == 0) atomicOr(a.err, 2u);
+                    break;
                 }
-                break;
+#ifdef LSMB_STATS
+                if (lane == 0) atomicAdd(a.err + 10, 1u);
+#endif
+                retry_deferred(a, L, w, lane, qn, dkey, doff, dmask);
+                flush_queue(a, L, w, lane, qn);
+                if (spin) __builtin_amdgcn_s_sleep(2);
             }
-            backoff(idle++);
         }
     }
-    __syncthreads();
-    // Final partial segments, padded with copies of their first offset
-    // (setting a bit twice is a no-op), then the per-region segment counts.
-    for (uint32_t lb = tid; lb < a.nb; lb += kBinBlock) {
-        const uint32_t f = claims[lb];
-        uint32_t c = cur[lb];
-        if (f) {
-            const uint32_t* sl = slots + lb * kSegEntries;
-            write_segment(a, [&](int e) { return (uint32_t)e < f ? sl[e] : sl[0]; }, a.b0 + lb, w, c);
-            c++;
+    // Drain: complete every deferred claim.
+    for (uint32_t spin = 0; __ballot(dmask != 0); spin++) {
+        if (spin == LSMB_SPIN_LIMIT) {
+            if (lane == 0) atomicOr(a.err, 4u);
+            break;
         }
-        a.counts[(uint64_t)(a.b0 + lb) * a.grid + w] = min(c, a.cap);
+        retry_deferred(a, L, w, lane, qn, dkey, doff, dmask);
+        flush_queue(a, L, w, lane, qn);
+        if (spin) __builtin_amdgcn_s_sleep(2);
+    }
+    __syncthreads();
+    // The open segment of each slice (claims % 24 entries), padded with
+    // copies of its first offset (setting a bit twice is a no-op), then the
+    // per-region segment counts.
+    for (uint32_t lb = tid; lb < a.nb; lb += kBinBlock) {
+        const uint32_t c = min(L.state[lb] & 0xFFFFu, climit);
+        const uint32_t sg = c / (uint32_t)kSegEntries, r = c % (uint32_t)kSegEntries;
+        if (r) {
+            uint64_t words[kSegWords];
+            const uint64_t* hp = L.half + lb * 16 + (sg & 1) * 8;
+            for (int j = 0; j < kSegWords; j++) words[j] = hp[j];
+            const uint64_t first = words[0] & kSliceMask;
+            for (uint32_t e = r; e < (uint32_t)kSegEntries; e++) words[e & 7] |= first << (20 * (e >> 3));
+            write_segment(a, words, a.b0 + lb, w, sg);
+        }
+        a.counts[(uint64_t)(a.b0 + lb) * a.grid + w] = sg + (r ? 1u : 0u);
     }
 }
 
@@ -484,7 +526,7 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
             a.counts = ws.counts;
             a.gw = gw;
             a.err = ws.err;
-            const size_t smem = (size_t)a.nb * kLdsBytesPerBin + (kBinBlock / 64) * 16 * 4;
+            const size_t smem = (size_t)a.nb * kLdsBytesPerBin + (kBinBlock / 64) * kQueue * 4;  // + flush queues
             auto go = [&](auto kern) {
                 hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
                 kern<<<dim3(pl.grid), dim3(kBinBlock), smem, st>>>(src, n, md, k, a);
@@ -538,7 +580,7 @@ BuildStrategy pick_build_strategy(uint32_t num_bits, uint32_t k, uint64_t n) {
 PartitionPlan plan_partition(uint32_t num_bits, uint32_t k, uint64_t n, int num_cus) {
     PartitionPlan pl;
     pl.nbins = (uint32_t)(((uint64_t)num_bits + kSliceMask) >> kSliceLog2);
-    // <= 1536 slices per sweep keeps a pass A workgroup within 150 KiB of
+    // <= kMaxBinsPerSweep slices per sweep keep a pass A workgroup within its
     // LDS (one 1024-thread workgroup per CU); bigger filters take more sweeps
     // (each re-reads and re-hashes the keys, and keeps only its slices).
     pl.sweeps = (pl.nbins + kMaxBinsPerSweep - 1) / kMaxBinsPerSweep;
@@ -556,7 +598,9 @@ PartitionPlan plan_partition(uint32_t num_bits, uint32_t k, uint64_t n, int num_
     const double mu = (double)keys_w * k * p;
     const double cap_e = mu + 8.0 * sqrt(mu) + 2.0 * kSegEntries;
     pl.cap_segs = (uint32_t)ceil(cap_e / kSegEntries);
-    pl.region_bytes = (uint64_t)pl.nbins * pl.grid * pl.cap_segs * 64;
+    // A region holds at most kMaxRegionSegs segments (pass A's state word);
+    // a bigger plan is reported as unbounded so callers chunk the keys.
+    pl.region_bytes = pl.cap_segs > kMaxRegionSegs ? ~0ull >> 2 : (uint64_t)pl.nbins * pl.grid * pl.cap_segs * 64;
     pl.counts_bytes = (uint64_t)pl.nbins * pl.grid * 4;
     return pl;
 }

@@ -106,6 +106,63 @@ __global__ __launch_bounds__(256) void k_probe_generic(Src src, uint64_t n,
     }
 }
 
+// Lexicographic byte-string order, as Rust's `[u8]` Ord (a proper prefix
+// sorts first): <0, 0, >0.
+__device__ __forceinline__ int key_cmp(const uint8_t* a, uint64_t la, const uint8_t* b, uint32_t lb) {
+    const uint64_t m = la < lb ? la : lb;
+    for (uint64_t i = 0; i < m; i++)
+        if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
+    return la < lb ? -1 : (la > lb ? 1 : 0);
+}
+
+// Filter-set probe (multi-get pre-check): per key, for every SSTable of the
+// set, the two checks SSTable::get makes before touching the index
+// (src/sstable/reader.rs:192-199): key inside [min_key, max_key], then
+// bloom.may_contain(key).  One hash per key; descriptors staged in LDS.
+template <class Src>
+__global__ __launch_bounds__(256) void k_fset_probe(Src src, uint64_t n, const RangedFilter* __restrict__ filters,
+                                                    uint32_t nfilt, uint64_t* __restrict__ out) {
+    __shared__ RangedFilter fl[64];
+    for (uint32_t f = threadIdx.x; f < nfilt; f += blockDim.x) fl[f] = filters[f];
+    __syncthreads();
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
+        const H128 h = src.hash(i);
+        const uint8_t* kp = src.bytes(i);
+        const uint64_t kl = src.key_len(i);
+        uint64_t m = 0;
+        for (uint32_t f = 0; f < nfilt; f++) {
+            const RangedFilter& R = fl[f];
+            if (key_cmp(kp, kl, R.lo, R.lo_len) < 0 || key_cmp(kp, kl, R.hi, R.hi_len) > 0) continue;
+            bool hit = true;
+            if (R.f.k) {
+                PosWalk pw(R.f.md, h.lo, h.hi);
+                for (uint32_t j = 0; j < R.f.k; j++) {
+                    const uint32_t p = pw.pos();
+                    if (!((R.f.words32[p >> 5] >> (p & 31)) & 1u)) {
+                        hit = false;
+                        break;
+                    }
+                    pw.next(R.f.md);
+                }
+            }
+            if (hit) m |= 1ull << R.f.out_bit;
+        }
+        out[i] = m;
+    }
+}
+
+template <class Src>
+hipError_t fset_probe_with(const Src& src, uint64_t n, const RangedFilter* df, uint32_t nfilt, uint64_t* out,
+                           int num_cus, hipStream_t st) {
+    uint64_t g = (n + 255) / 256;
+    const uint64_t gmax = (uint64_t)num_cus * 8;
+    if (g > gmax) g = gmax;
+    if (g < 1) g = 1;
+    k_fset_probe<Src><<<dim3((uint32_t)g), dim3(256), 0, st>>>(src, n, df, nfilt, out);
+    return hipGetLastError();
+}
+
 template <class Src>
 hipError_t probe_with(const Src& src, uint64_t n, const ProbeFilter* hf, uint32_t nfilt,
                       const ProbeFilter* df, uint8_t* out, int num_cus, hipStream_t st) {
@@ -139,6 +196,16 @@ hipError_t probe_with(const Src& src, uint64_t n, const ProbeFilter* hf, uint32_
 }
 
 }  // namespace
+
+hipError_t launch_fset_probe(const KeyBatch& kb, const RangedFilter* df, uint32_t nfilt, uint64_t* out,
+                             int num_cus, hipStream_t st) {
+    if (kb.n == 0) return hipSuccess;
+    if (nfilt > 64) return hipErrorInvalidValue;
+    if (kb.offsets) return fset_probe_with(VarLen{kb.data, kb.offsets}, kb.n, df, nfilt, out, num_cus, st);
+    if (kb.key_len == 16 && (reinterpret_cast<uintptr_t>(kb.data) & 15) == 0)
+        return fset_probe_with(Fixed16{reinterpret_cast<const uint4*>(kb.data)}, kb.n, df, nfilt, out, num_cus, st);
+    return fset_probe_with(FixedN{kb.data, kb.key_len}, kb.n, df, nfilt, out, num_cus, st);
+}
 
 hipError_t launch_probe(const KeyBatch& kb, const ProbeFilter* hf, uint32_t nfilt,
                         ProbeFilter* df, uint8_t* out, int num_cus, hipStream_t st) {

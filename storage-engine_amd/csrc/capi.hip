@@ -129,9 +129,9 @@ int check_device_error(lsmb_ctx* c) {
     {
         uint32_t st[16];
         HIP_TRY(hipMemcpy(st, c->err.p, 64, hipMemcpyDeviceToHost));
-        fprintf(stderr, "[lsmb stats] void=%u retry_wave_iters=%u wave_iters=%u retry_loop_iters=%u\n", st[9], st[10],
-                st[11], st[12]);
-        HIP_TRY(hipMemset((char*)c->err.p + 36, 0, 28));
+        fprintf(stderr, "[lsmb stats] deferred=%u region_full=%u stall_passes=%u wave_iters=%u flush_rounds=%u\n",
+                st[9], st[7], st[10], st[11], st[12]);
+        HIP_TRY(hipMemset((char*)c->err.p + 4, 0, 60));
     }
 #endif
     HIP_TRY(hipMemcpy(c->err_host, c->err.p, 32, hipMemcpyDeviceToHost));
@@ -451,6 +451,29 @@ int lsmb_build_var(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, ui
     return check_device_error(c);
 }
 
+// Copies a host key batch into the context's staging buffers (ctx stream).
+static int stage_host_keys(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
+                           KeyBatch* kb) {
+    uint64_t kbytes;
+    if (offsets) {
+        for (uint64_t i = 0; i < n; i++)
+            if (offsets[i + 1] < offsets[i]) return fail(LSMB_EINVAL, "offsets not non-decreasing");
+        kbytes = offsets[n] - offsets[0];
+        c->offs_tmp.resize(n + 1);
+        for (uint64_t i = 0; i <= n; i++) c->offs_tmp[i] = offsets[i] - offsets[0];
+        HIP_TRY(c->offs.ensure((n + 1) * 8));
+        HIP_TRY(hipMemcpyAsync(c->offs.p, c->offs_tmp.data(), (n + 1) * 8, hipMemcpyHostToDevice, c->st));
+        HIP_TRY(c->keys.ensure(kbytes + 16));
+        if (kbytes) HIP_TRY(hipMemcpyAsync(c->keys.p, data + offsets[0], kbytes, hipMemcpyHostToDevice, c->st));
+    } else {
+        kbytes = (uint64_t)key_len * n;
+        HIP_TRY(c->keys.ensure(kbytes + 16));
+        if (kbytes) HIP_TRY(hipMemcpyAsync(c->keys.p, data, kbytes, hipMemcpyHostToDevice, c->st));
+    }
+    *kb = KeyBatch{(const uint8_t*)c->keys.p, offsets ? (const uint64_t*)c->offs.p : nullptr, key_len, n};
+    return LSMB_OK;
+}
+
 static int probe_common(lsmb_ctx* c, const uint32_t* const* wptrs, const uint32_t* filt_bits,
                         const uint32_t* filt_k, uint32_t nfilt, const KeyBatch& kb, uint8_t* d_out,
                         hipStream_t st) {
@@ -524,23 +547,8 @@ int lsmb_probe(lsmb_ctx* c, const uint64_t* const* filt_words, const uint32_t* f
     }
     const uint32_t stride = (nfilt + 7) / 8;
     HIP_TRY(c->out.ensure(n * stride));
-    uint64_t kbytes;
-    if (offsets) {
-        for (uint64_t i = 0; i < n; i++)
-            if (offsets[i + 1] < offsets[i]) return fail(LSMB_EINVAL, "offsets not non-decreasing");
-        kbytes = offsets[n] - offsets[0];
-        c->offs_tmp.resize(n + 1);
-        for (uint64_t i = 0; i <= n; i++) c->offs_tmp[i] = offsets[i] - offsets[0];
-        HIP_TRY(c->offs.ensure((n + 1) * 8));
-        HIP_TRY(hipMemcpyAsync(c->offs.p, c->offs_tmp.data(), (n + 1) * 8, hipMemcpyHostToDevice, c->st));
-        HIP_TRY(c->keys.ensure(kbytes + 16));
-        if (kbytes) HIP_TRY(hipMemcpyAsync(c->keys.p, data + offsets[0], kbytes, hipMemcpyHostToDevice, c->st));
-    } else {
-        kbytes = (uint64_t)key_len * n;
-        HIP_TRY(c->keys.ensure(kbytes + 16));
-        if (kbytes) HIP_TRY(hipMemcpyAsync(c->keys.p, data, kbytes, hipMemcpyHostToDevice, c->st));
-    }
-    KeyBatch kb{(const uint8_t*)c->keys.p, offsets ? (const uint64_t*)c->offs.p : nullptr, key_len, n};
+    KeyBatch kb;
+    if (int rc = stage_host_keys(c, data, offsets, key_len, n, &kb)) return rc;
     if (int rc = probe_common(c, dptr.data(), filt_bits, filt_k, nfilt, kb, (uint8_t*)c->out.p, c->st)) return rc;
     HIP_TRY(hipMemcpyAsync(out, c->out.p, n * stride, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(hipStreamSynchronize(c->st));
@@ -577,6 +585,185 @@ int lsmb_last_build_ms(lsmb_ctx* c, float* out3) {
     HIP_TRY(hipEventElapsedTime(&out3[0], c->tm.t0, c->tm.t2));
     HIP_TRY(hipEventElapsedTime(&out3[1], c->tm.t0, c->tm.t1));
     HIP_TRY(hipEventElapsedTime(&out3[2], c->tm.t1, c->tm.t2));
+    return LSMB_OK;
+}
+
+// ---------------------------------------------------------------- filter sets
+// A device-resident set of up to 64 SSTable filters with their key ranges:
+// the multi-get pre-check of DB::get (src/db/mod.rs:243-267 -> SSTable::get,
+// src/sstable/reader.rs:192-199), without re-opening and re-deserializing
+// every table per lookup (mod.rs:245,259).
+struct lsmb_fset {
+    lsmb_ctx* c = nullptr;
+    struct Slot {
+        bool live = false;
+        DevBuf words;
+        uint32_t num_bits = 0, k = 0;
+        std::vector<uint8_t> lo, hi;
+    };
+    Slot slot[64];
+    DevBuf ranges;  // every live slot's lo and hi keys
+    DevBuf desc;    // RangedFilter[ndesc]
+    uint32_t ndesc = 0;
+    bool dirty = true;
+};
+
+namespace {
+
+// Rebuilds the device descriptors after an add/remove (rare; probes re-use them).
+int fset_refresh(lsmb_fset* fs) {
+    if (!fs->dirty) return LSMB_OK;
+    std::vector<uint8_t> blob;
+    std::vector<RangedFilter> d;
+    std::vector<std::pair<uint64_t, uint64_t>> at;  // blob offsets of lo, hi
+    for (uint32_t s = 0; s < 64; s++) {
+        const auto& S = fs->slot[s];
+        if (!S.live) continue;
+        at.push_back({blob.size(), blob.size() + S.lo.size()});
+        blob.insert(blob.end(), S.lo.begin(), S.lo.end());
+        blob.insert(blob.end(), S.hi.begin(), S.hi.end());
+    }
+    HIP_TRY(hipDeviceSynchronize());  // no probe may still read the old descriptors
+    HIP_TRY(fs->ranges.ensure(std::max<size_t>(blob.size(), 16)));
+    if (!blob.empty()) HIP_TRY(hipMemcpy(fs->ranges.p, blob.data(), blob.size(), hipMemcpyHostToDevice));
+    const uint8_t* rb = (const uint8_t*)fs->ranges.p;
+    uint32_t j = 0;
+    for (uint32_t s = 0; s < 64; s++) {
+        const auto& S = fs->slot[s];
+        if (!S.live) continue;
+        RangedFilter r;
+        memset(&r, 0, sizeof r);
+        r.f.words32 = (const uint32_t*)S.words.p;
+        r.f.md = Mod32::make(S.num_bits ? S.num_bits : 1);
+        r.f.num_bits = S.num_bits;
+        r.f.k = S.k;
+        r.f.out_bit = s;
+        r.f.group = s;
+        r.lo = rb + at[j].first;
+        r.hi = rb + at[j].second;
+        r.lo_len = (uint32_t)S.lo.size();
+        r.hi_len = (uint32_t)S.hi.size();
+        d.push_back(r);
+        j++;
+    }
+    HIP_TRY(fs->desc.ensure(sizeof(RangedFilter) * 64));
+    if (!d.empty()) HIP_TRY(hipMemcpy(fs->desc.p, d.data(), sizeof(RangedFilter) * d.size(), hipMemcpyHostToDevice));
+    fs->ndesc = (uint32_t)d.size();
+    fs->dirty = false;
+    return LSMB_OK;
+}
+
+int fset_add_common(lsmb_fset* fs, const uint8_t* words_le, uint32_t num_bits, uint32_t k, const uint8_t* min_key,
+                    uint64_t min_len, const uint8_t* max_key, uint64_t max_len) {
+    if (int rc = check_filter(num_bits, k)) return rc;
+    if ((min_len && !min_key) || (max_len && !max_key)) return fail(LSMB_EINVAL, "null key range");
+    if (min_len > UINT32_MAX || max_len > UINT32_MAX) return fail(LSMB_EINVAL, "range key too long");
+    int s = 0;
+    while (s < 64 && fs->slot[s].live) s++;
+    if (s == 64) return fail(LSMB_EINVAL, "filter set full (64 filters)");
+    DevGuard g(fs->c->dev);
+    auto& S = fs->slot[s];
+    const uint64_t nw = nwords64(num_bits);
+    HIP_TRY(hipDeviceSynchronize());  // the slot's old buffer may still be read by a probe
+    HIP_TRY(S.words.ensure(std::max<uint64_t>(nw, 2) * 8));
+    if (nw) HIP_TRY(hipMemcpy(S.words.p, words_le, nw * 8, hipMemcpyHostToDevice));
+    S.num_bits = num_bits;
+    S.k = k;
+    S.lo.assign(min_key, min_key + min_len);
+    S.hi.assign(max_key, max_key + max_len);
+    S.live = true;
+    fs->dirty = true;
+    return s;
+}
+
+}  // namespace
+
+int lsmb_fset_open(lsmb_ctx* c, lsmb_fset** out) {
+    if (!c || !out) return fail(LSMB_EINVAL, "null argument");
+    *out = new lsmb_fset;
+    (*out)->c = c;
+    return LSMB_OK;
+}
+
+void lsmb_fset_close(lsmb_fset* fs) {
+    if (!fs) return;
+    {
+        DevGuard g(fs->c->dev);
+        hipDeviceSynchronize();
+        for (auto& S : fs->slot) S.words.release();
+        fs->ranges.release();
+        fs->desc.release();
+    }
+    delete fs;
+}
+
+int lsmb_fset_add(lsmb_fset* fs, const uint8_t* block, uint64_t len, const uint8_t* min_key, uint64_t min_len,
+                  const uint8_t* max_key, uint64_t max_len) {
+    if (!fs) return fail(LSMB_EINVAL, "null filter set");
+    uint32_t k, nb, nw;
+    if (int rc = lsmb_deserialize_header(block, len, &k, &nb, &nw)) return rc;
+    return fset_add_common(fs, block + 12, nb, k, min_key, min_len, max_key, max_len);
+}
+
+int lsmb_fset_add_words(lsmb_fset* fs, const uint64_t* words, uint32_t num_bits, uint32_t num_hashes,
+                        const uint8_t* min_key, uint64_t min_len, const uint8_t* max_key, uint64_t max_len) {
+    if (!fs) return fail(LSMB_EINVAL, "null filter set");
+    if (!words && nwords64(num_bits)) return fail(LSMB_EINVAL, "null words");
+    return fset_add_common(fs, (const uint8_t*)words, num_bits, num_hashes, min_key, min_len, max_key, max_len);
+}
+
+int lsmb_fset_remove(lsmb_fset* fs, int slot) {
+    if (!fs) return fail(LSMB_EINVAL, "null filter set");
+    if (slot < 0 || slot >= 64 || !fs->slot[slot].live) return fail(LSMB_EINVAL, "no filter in slot %d", slot);
+    fs->slot[slot].live = false;  // the buffer is re-used by a later add
+    fs->dirty = true;
+    return LSMB_OK;
+}
+
+uint64_t lsmb_fset_live_mask(const lsmb_fset* fs) {
+    uint64_t m = 0;
+    if (fs)
+        for (int s = 0; s < 64; s++)
+            if (fs->slot[s].live) m |= 1ull << s;
+    return m;
+}
+
+int lsmb_fset_probe_dev(lsmb_fset* fs, const void* d_data, const void* d_offsets, uint32_t key_len, uint64_t n,
+                        void* d_out, void* stream) {
+    if (!fs) return fail(LSMB_EINVAL, "null filter set");
+    if (n == 0) return LSMB_OK;
+    if (!d_out || !d_data) return fail(LSMB_EINVAL, "null keys or output");
+    DevGuard g(fs->c->dev);
+    if (int rc = fset_refresh(fs)) return rc;
+    const hipStream_t st = pick_stream(fs->c, stream);
+    if (fs->ndesc == 0) {
+        HIP_TRY(hipMemsetAsync(d_out, 0, n * 8, st));
+        return LSMB_OK;
+    }
+    KeyBatch kb{(const uint8_t*)d_data, (const uint64_t*)d_offsets, key_len, n};
+    HIP_TRY(launch_fset_probe(kb, (const RangedFilter*)fs->desc.p, fs->ndesc, (uint64_t*)d_out, fs->c->num_cus, st));
+    return LSMB_OK;
+}
+
+int lsmb_fset_probe(lsmb_fset* fs, const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
+                    uint64_t* out_mask) {
+    if (!fs) return fail(LSMB_EINVAL, "null filter set");
+    if (n == 0) return LSMB_OK;
+    if (!out_mask || (!data && (offsets ? offsets[n] > offsets[0] : key_len > 0)))
+        return fail(LSMB_EINVAL, "null keys or output");
+    lsmb_ctx* c = fs->c;
+    DevGuard g(c->dev);
+    if (int rc = fset_refresh(fs)) return rc;
+    HIP_TRY(c->out.ensure(n * 8));
+    KeyBatch kb;
+    if (int rc = stage_host_keys(c, data, offsets, key_len, n, &kb)) return rc;
+    if (fs->ndesc == 0) {
+        memset(out_mask, 0, n * 8);
+        return LSMB_OK;
+    }
+    HIP_TRY(launch_fset_probe(kb, (const RangedFilter*)fs->desc.p, fs->ndesc, (uint64_t*)c->out.p, c->num_cus, c->st));
+    HIP_TRY(hipMemcpyAsync(out_mask, c->out.p, n * 8, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
     return LSMB_OK;
 }
 

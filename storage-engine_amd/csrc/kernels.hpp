@@ -17,8 +17,9 @@ constexpr int kSegWords = 8;                          // 3 offsets per u64 word
 constexpr int kBinBlock = 1024;                       // pass A workgroup
 constexpr int kApplyBlock = 1024;                     // pass B workgroup
 constexpr uint32_t kLdsFilterMaxWords32 = 40 * 1024;  // 160 KiB: whole filter in LDS
-constexpr uint32_t kLdsBytesPerBin = kSegEntries * 4 + 12;  // 24 slots + claims/done/cursor
-constexpr uint32_t kMaxBinsPerSweep = 1380;                // <= 149 KiB of pass A LDS (+ 1 KiB flush queues)
+constexpr uint32_t kLdsBytesPerBin = 2 * kSegWords * 8 + 4 + 4;  // two packed segments + state + done
+constexpr uint32_t kMaxBinsPerSweep = 1152;                // <= 153 KiB of pass A LDS (+ 4 KiB flush queues)
+constexpr uint32_t kMaxRegionSegs = 510;                  // pass A state: claims < 2^16, gens < 2^8
 
 // How a key batch is presented to the kernels.
 struct KeyBatch {
@@ -81,6 +82,20 @@ struct ProbeFilter {
     uint32_t out_bit;  // bit index in the output mask row
     uint32_t group;    // filters with equal (num_bits, k) share one position walk
 };
+
+// A filter of a filter set (lsmb_fset): the SSTable's filter plus its key
+// range [lo, hi] (SSTable meta min_key/max_key, src/sstable/reader.rs:192).
+struct RangedFilter {
+    ProbeFilter f;  // f.out_bit = the slot
+    const uint8_t* lo;
+    const uint8_t* hi;
+    uint32_t lo_len, hi_len;
+};
+
+// out[i] bit s = (lo_s <= key i <= hi_s) && may_contain(filter s, key i), for
+// the nfilt (<= 64) descriptors at d_filters (device memory).
+hipError_t launch_fset_probe(const KeyBatch& kb, const RangedFilter* d_filters, uint32_t nfilt, uint64_t* d_out,
+                             int num_cus, hipStream_t st);
 
 hipError_t launch_probe(const KeyBatch& kb, const ProbeFilter* h_filters, uint32_t nfilt,
                         ProbeFilter* d_filters_scratch, uint8_t* d_out, int num_cus,

@@ -23,6 +23,8 @@ struct Fixed16 {
         uint4 v = ld_stream16(k + i);
         return xxh3_16(((uint64_t)v.y << 32) | v.x, ((uint64_t)v.w << 32) | v.z);
     }
+    __device__ __forceinline__ const uint8_t* bytes(uint64_t i) const { return reinterpret_cast<const uint8_t*>(k + i); }
+    __device__ __forceinline__ uint64_t key_len(uint64_t) const { return 16; }
 };
 
 // Any fixed key length, any alignment.
@@ -30,6 +32,8 @@ struct FixedN {
     const uint8_t* d;
     uint32_t len;
     __device__ __forceinline__ H128 hash(uint64_t i) const { return xxh3_128(d + i * len, len); }
+    __device__ __forceinline__ const uint8_t* bytes(uint64_t i) const { return d + i * len; }
+    __device__ __forceinline__ uint64_t key_len(uint64_t) const { return len; }
 };
 
 // Packed variable-length keys: key i = d[o[i] .. o[i+1]).
@@ -40,6 +44,8 @@ struct VarLen {
         uint64_t a = o[i], b = o[i + 1];
         return xxh3_128(d + a, b - a);
     }
+    __device__ __forceinline__ const uint8_t* bytes(uint64_t i) const { return d + o[i]; }
+    __device__ __forceinline__ uint64_t key_len(uint64_t i) const { return o[i + 1] - o[i]; }
 };
 
 }  // namespace ks

@@ -19,7 +19,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "liblsmbloom.so")
+LIB_PATH = os.environ.get("LSMB_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "liblsmbloom.so")  # LSMB_LIB: instrumented builds (tools/)
 
 LSMB_OK = 0
 LSMB_EINVAL = -1
@@ -62,6 +62,15 @@ SIGNATURES = {
                                       ctypes.c_uint32, ctypes.c_uint64, vp, vp]),
     "lsmb_or_reduce_dev": (ctypes.c_int, [vp, vp, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, vp]),
     "lsmb_gen_key16_dev": (ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, vp, vp]),
+    "lsmb_fset_open": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
+    "lsmb_fset_close": (None, [vp]),
+    "lsmb_fset_add": (ctypes.c_int, [vp, u8p, ctypes.c_uint64, u8p, ctypes.c_uint64, u8p, ctypes.c_uint64]),
+    "lsmb_fset_add_words": (ctypes.c_int, [vp, u64p, ctypes.c_uint32, ctypes.c_uint32, u8p, ctypes.c_uint64, u8p,
+                                           ctypes.c_uint64]),
+    "lsmb_fset_remove": (ctypes.c_int, [vp, ctypes.c_int]),
+    "lsmb_fset_live_mask": (ctypes.c_uint64, [vp]),
+    "lsmb_fset_probe": (ctypes.c_int, [vp, u8p, u64p, ctypes.c_uint32, ctypes.c_uint64, u64p]),
+    "lsmb_fset_probe_dev": (ctypes.c_int, [vp, vp, vp, ctypes.c_uint32, ctypes.c_uint64, vp, vp]),
     "lsmb_build_strategy": (ctypes.c_char_p, [ctypes.c_uint32, ctypes.c_uint64]),
     "lsmb_last_build_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_float)]),
 }
@@ -247,6 +256,83 @@ class Context:
         a = (ctypes.c_float * 3)()
         _check(lib().lsmb_last_build_ms(self.h, a))
         return tuple(a)
+
+
+class FilterSet:
+    """Device-resident SSTable filters with key ranges (lsmb_fset): the batched
+    form of SSTable::get's range + bloom pre-check (src/sstable/reader.rs:192-199).
+
+    probe(keys)[i] bit s = (min_s <= key_i <= max_s) and may_contain(filter s, key_i).
+    """
+
+    def __init__(self, ctx=None):
+        self.ctx = ctx or default_context()
+        h = vp()
+        _check(lib().lsmb_fset_open(self.ctx.h, ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            lib().lsmb_fset_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def add(self, block, min_key, max_key):
+        """block: serialized filter bytes (BloomFilter::serialize) -> slot."""
+        b, n = _key(block)
+        lo, nlo = _key(min_key)
+        hi, nhi = _key(max_key)
+        return _check(lib().lsmb_fset_add(self.h, _p(b, u8p), n, _p(lo, u8p), nlo, _p(hi, u8p), nhi))
+
+    def add_filter(self, filt, min_key, max_key):
+        """filt: BloomFilter -> slot."""
+        w = np.ascontiguousarray(filt.bits, dtype=np.uint64)
+        if w.size == 0:
+            w = np.zeros(1, np.uint64)
+        lo, nlo = _key(min_key)
+        hi, nhi = _key(max_key)
+        return _check(lib().lsmb_fset_add_words(self.h, _p(w, u64p), filt.num_bits(), filt.num_hashes(),
+                                                _p(lo, u8p), nlo, _p(hi, u8p), nhi))
+
+    def remove(self, slot):
+        _check(lib().lsmb_fset_remove(self.h, int(slot)))
+
+    def live_mask(self):
+        return int(lib().lsmb_fset_live_mask(self.h))
+
+    def probe(self, data, offsets=None, key_len=0):
+        """Packed host keys (as Context.probe) -> uint64 mask per key."""
+        data = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+        if offsets is not None:
+            offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+            n = offsets.size - 1
+            op = _p(offsets, u64p)
+        else:
+            n = data.size // key_len if key_len else 0
+            op = None
+        out = np.zeros(n, dtype=np.uint64)
+        if data.size == 0:
+            data = np.zeros(1, np.uint8)
+        _check(lib().lsmb_fset_probe(self.h, _p(data, u8p), op, key_len, n, _p(out if n else np.zeros(1, np.uint64),
+                                                                                u64p)))
+        return out
+
+    def probe_keys(self, keys):
+        """list of bytes -> uint64 mask per key."""
+        lens = np.array([len(k) for k in keys], dtype=np.uint64)
+        offs = np.zeros(len(keys) + 1, dtype=np.uint64)
+        np.cumsum(lens, out=offs[1:])
+        return self.probe(np.frombuffer(b"".join(bytes(k) for k in keys), dtype=np.uint8), offs)
+
+    def probe_dev(self, data, n, out, offsets=None, key_len=0, stream=None):
+        _check(lib().lsmb_fset_probe_dev(self.h, vp(data.data_ptr()),
+                                         vp(offsets.data_ptr()) if offsets is not None else None, key_len, n,
+                                         vp(out.data_ptr()), Context._stream(stream)))
 
 
 def build_strategy(num_bits, n):

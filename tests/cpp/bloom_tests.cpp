@@ -15,6 +15,7 @@
 using lsm::bloom::BloomFilter;
 using lsm::bloom::BloomFilterBuilder;
 using lsm::bloom::Corruption;
+using lsm::bloom::FilterSet;
 
 static int g_fail = 0, g_run = 0;
 #define CHECK(c)                                                              \
@@ -234,6 +235,27 @@ int main(int argc, char** argv) {
                 fp += m[i] & 1;
             }
             CHECK(fp == 106);  // golden: bloom_kats.json "sstable_exist_fpr"
+        });
+        run("filter set: range check then bloom check (reader.rs:192-199)", [] {
+            FilterSet fs;
+            BloomFilter a(1000, 0.01), b(1000, 0.01);
+            char k[16];
+            for (int i = 0; i < 100; i++) {
+                snprintf(k, sizeof k, "key_%05d", i);
+                a.insert(k);
+                snprintf(k, sizeof k, "key_%05d", 1000 + i);
+                b.insert(k);
+            }
+            const int sa = fs.add(a.serialize(), "key_00000", "key_00099");
+            const int sb = fs.add(b, "key_01000", "key_01099");
+            CHECK(fs.live_mask() == ((1ull << sa) | (1ull << sb)));
+            const std::vector<std::string> q = {"key_00000", "key_00099", "key_01050", "key_00500", "key_0", "", "zz"};
+            auto m = fs.probe(q);
+            CHECK(m[0] == (1ull << sa) && m[1] == (1ull << sa) && m[2] == (1ull << sb));
+            CHECK(m[3] == 0 && m[4] == 0 && m[5] == 0 && m[6] == 0);  // outside every range
+            CHECK(throws<Corruption>([&] { fs.add(std::vector<uint8_t>{1, 2, 3}, "a", "b"); }));
+            fs.remove(sa);
+            CHECK(fs.probe({"key_00000"})[0] == 0);
         });
     }
     printf("%d/%d passed\n", g_run - g_fail, g_run);

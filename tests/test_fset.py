@@ -1,0 +1,164 @@
+"""Device-resident filter sets (lsmb_fset): the batched form of the two checks
+SSTable::get makes before reading the index (src/sstable/reader.rs:192-199):
+
+    min_key <= key <= max_key  (Rust [u8] Ord: byte-wise, a proper prefix first)
+    && bloom.may_contain(key)
+
+Expected answers come from the CPU oracle's may_contain (the checker) and
+Python's bytes ordering, which is the same lexicographic order as Rust's.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import keygen
+import lsmbloom
+from lsmbloom import BloomFilter, FilterSet
+
+
+def expected_masks(oracle, tables, keys):
+    """tables: {slot: (words, num_bits, k, lo, hi)} -> list of uint64 masks."""
+    data, offs = keygen.pack(keys)
+    out = [0] * len(keys)
+    for s, (w, nb, k, lo, hi) in tables.items():
+        hit = oracle.probe([(w, nb, k)], data, offsets=offs)[:, 0]
+        for i, key in enumerate(keys):
+            if hit[i] and lo <= key <= hi:
+                out[i] |= 1 << s
+    return out
+
+
+def sst_tables(oracle, ntab, per, seed):
+    """ntab SSTable-like runs of `per` sorted keys each (L0-style overlapping
+    ranges for even tables, disjoint for odd ones), filters sized as
+    SSTableBuilder::with_estimated_keys(per) does (src/sstable/builder.rs:74)."""
+    rng = np.random.default_rng(seed)
+    tabs = []
+    for t in range(ntab):
+        base = t * 10_000 if t % 2 else (t // 2) * 3_000
+        ids = np.sort(rng.choice(20_000, size=per, replace=False)) + base
+        keys = [b"user%08d" % i for i in ids]
+        nb, k = lsmbloom.params(per, 0.01)
+        data, offs = keygen.pack(keys)
+        w = oracle.build_var(data, offs, nb, k)
+        tabs.append((keys, w, nb, k))
+    return tabs
+
+
+def test_fset_open_without_context_is_einval():
+    h = ctypes.c_void_p()
+    assert lsmbloom.lib().lsmb_fset_open(None, ctypes.byref(h)) == lsmbloom.LSMB_EINVAL
+    assert lsmbloom.lib().lsmb_fset_live_mask(None) == 0
+
+
+@pytest.mark.gpu
+def test_fset_matches_range_and_bloom_checks(oracle):
+    ctx = lsmbloom.Context(0)
+    fs = FilterSet(ctx)
+    tabs = sst_tables(oracle, 12, 1000, 7)
+    tables = {}
+    for keys, w, nb, k in tabs:
+        s = fs.add(oracle.serialize(w, nb, k), keys[0], keys[-1])
+        tables[s] = (w, nb, k, keys[0], keys[-1])
+    assert fs.live_mask() == (1 << len(tabs)) - 1
+    rng = np.random.default_rng(11)
+    q = [kk for keys, _, _, _ in tabs for kk in keys[::7]]                     # members
+    q += [b"user%08d" % i for i in rng.integers(0, 140_000, 20_000)]          # mostly absent
+    q += [keys[0] for keys, *_ in tabs] + [keys[-1] for keys, *_ in tabs]     # inclusive bounds
+    q += [b"", b"user", b"user0", b"user00000000\x00", b"zzz", b"\xff" * 40]  # prefixes, extremes
+    q += [keys[0][:-1] for keys, *_ in tabs] + [keys[-1] + b"\x00" for keys, *_ in tabs]
+    got = fs.probe_keys(q)
+    exp = expected_masks(oracle, tables, q)
+    assert [int(x) for x in got] == exp
+    # every member is reported by its own table
+    for s, (keys, *_rest) in enumerate(tabs):
+        m = fs.probe_keys(keys)
+        assert all(int(x) >> s & 1 for x in m)
+    fs.close()
+    ctx.close()
+
+
+@pytest.mark.gpu
+def test_fset_fixed_len_keys_and_device_probe(oracle):
+    import torch
+
+    ctx = lsmbloom.Context(0)
+    fs = FilterSet(ctx)
+    tables = {}
+    for t in range(8):
+        keys = keygen.key16(0x5EED0100 + t, 0, 5000)
+        rows = sorted(bytes(r) for r in keys)
+        nb, k = lsmbloom.params(5000, 0.01)
+        w = oracle.build_fixed(keys, 16, nb, k)
+        s = fs.add_filter(BloomFilter(w, k, nb), rows[len(rows) // 4], rows[3 * len(rows) // 4])
+        tables[s] = (w, nb, k, rows[len(rows) // 4], rows[3 * len(rows) // 4])
+    q = np.concatenate([keygen.key16(0x5EED0100 + t, 0, 3000) for t in range(8)]
+                       + [keygen.key16(0x5EED0200, 0, 20_000)])
+    got = fs.probe(q, key_len=16)
+    exp = expected_masks(oracle, tables, [bytes(r) for r in q])
+    assert [int(x) for x in got] == exp
+    dq = torch.from_numpy(np.ascontiguousarray(q)).to("cuda:0")
+    dout = torch.zeros(q.shape[0], dtype=torch.int64, device="cuda:0")
+    fs.probe_dev(dq, q.shape[0], dout, key_len=16)
+    torch.cuda.synchronize()
+    assert np.array_equal(dout.cpu().numpy().view(np.uint64), got)
+    # unaligned fixed-length keys (FixedN path)
+    q7 = np.ascontiguousarray(q[:5000, :7])
+    got7 = fs.probe(q7, key_len=7)
+    assert [int(x) for x in got7] == expected_masks(oracle, tables, [bytes(r) for r in q7])
+    fs.close()
+    ctx.close()
+
+
+@pytest.mark.gpu
+def test_fset_add_remove_reuse_and_limits(oracle):
+    ctx = lsmbloom.Context(0)
+    fs = FilterSet(ctx)
+    assert fs.probe_keys([b"a", b"b"]).tolist() == [0, 0]  # empty set
+    nb, k = lsmbloom.params(100, 0.01)
+    slots = []
+    for t in range(64):
+        w = np.zeros(lsmbloom.num_words(nb), np.uint64)
+        oracle.insert(w, nb, k, b"k%02d" % t)
+        slots.append(fs.add_filter(BloomFilter(w, k, nb), b"k%02d" % t, b"k%02d" % t))
+    assert slots == list(range(64))
+    with pytest.raises(ValueError):
+        fs.add_filter(BloomFilter(np.zeros(lsmbloom.num_words(nb), np.uint64), k, nb), b"", b"")
+    m = fs.probe_keys([b"k%02d" % t for t in range(64)])
+    assert [int(x) for x in m] == [1 << t for t in range(64)]
+    fs.remove(5)
+    fs.remove(40)
+    with pytest.raises(ValueError):
+        fs.remove(5)
+    assert fs.live_mask() == ((1 << 64) - 1) & ~(1 << 5) & ~(1 << 40)
+    assert int(fs.probe_keys([b"k05"])[0]) == 0
+    w = np.zeros(lsmbloom.num_words(nb), np.uint64)
+    oracle.insert(w, nb, k, b"new")
+    assert fs.add(oracle.serialize(w, nb, k), b"a", b"z") == 5  # lowest free slot
+    got = int(fs.probe_keys([b"new"])[0])
+    assert got >> 5 & 1 and not got >> 40 & 1
+    fs.close()
+    ctx.close()
+
+
+@pytest.mark.gpu
+def test_fset_add_rejects_corrupt_blocks_like_deserialize(oracle):
+    ctx = lsmbloom.Context(0)
+    fs = FilterSet(ctx)
+    nb, k = lsmbloom.params(100, 0.01)
+    good = oracle.serialize(np.zeros(lsmbloom.num_words(nb), np.uint64), nb, k)
+    for bad in (b"", b"\xff\xff\xff\xff", bytes([7, 0, 0, 0, 0xE8, 3, 0, 0, 100, 0, 0, 0]),
+                good + b"extra", good[:-1]):
+        with pytest.raises(lsmbloom.Corruption):
+            fs.add(bad, b"a", b"z")
+    assert fs.live_mask() == 0
+    # num_bits == 0 with k > 0: the reference would panic (% by zero) on probe
+    zero = bytes([7, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0])
+    with pytest.raises(ValueError):
+        fs.add(zero, b"a", b"z")
+    # k == 0: may_contain is vacuously true, so only the range decides
+    s = fs.add(bytes([0, 0, 0, 0]) + good[4:], b"b", b"c")
+    assert [int(x) for x in fs.probe_keys([b"a", b"b", b"bz", b"c", b"c\x00"])] == [0, 1 << s, 1 << s, 1 << s, 0]
+    fs.close()
+    ctx.close()

@@ -24,5 +24,5 @@ for n, nb, k in cfgs:
         st = "ok"
     except Exception as e:  # noqa: BLE001
         st = str(e)
-    print("n=%d nb=%d k=%d strategy=%s %.3fs %s" % (n, nb, k, lsmbloom.build_strategy(nb, n), time.time() - t0, st),
-          flush=True)
+    print("n=%d nb=%d k=%d strategy=%s %.3fs %s ms=%s" % (n, nb, k, lsmbloom.build_strategy(nb, n),
+                                                          time.time() - t0, st, ctx.last_build_ms()), flush=True)
