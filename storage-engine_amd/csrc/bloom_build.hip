@@ -256,8 +256,9 @@ __device__ __forceinline__ void retry_deferred(const PassA& a, const BinLds& L, 
 #endif
 
 // Pass A.  One key per lane per iteration; W = Walk32 when num_bits <= 2^31,
-// else Walk64.  KMAX bounds k.
-template <class Src, class W, int KMAX>
+// else Walk64.  KMAX bounds k.  FULL: this sweep covers every slice (no
+// per-position sweep check).
+template <class Src, class W, int KMAX, bool FULL>
 __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md, uint32_t k, PassA a) {
     extern __shared__ uint64_t smem64[];
     BinLds L;
@@ -292,10 +293,10 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
             for (int q = 0; q < KMAX; q++) {
                 if ((uint32_t)q < k) {
                     const uint32_t p = walk.pos();
-                    const uint32_t b = (p >> kSliceLog2) - a.b0;
+                    const uint32_t b = (p >> kSliceLog2) - (FULL ? 0u : a.b0);
                     lb[q] = b;
                     off[q] = p & kSliceMask;
-                    if (b < a.nb) pend |= 1u << q;
+                    if (FULL || b < a.nb) pend |= 1u << q;
                     walk.next(md);
                 }
             }
@@ -531,12 +532,17 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
                 hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
                 kern<<<dim3(pl.grid), dim3(kBinBlock), smem, st>>>(src, n, md, k, a);
             };
+            const bool full = pl.sweeps == 1;
             if (k <= 8) {
-                if (w32) go(k_bin<Src, Walk32, 8>); else go(k_bin<Src, Walk64, 8>);
+                if (w32) {
+                    if (full) go(k_bin<Src, Walk32, 8, true>); else go(k_bin<Src, Walk32, 8, false>);
+                } else {
+                    if (full) go(k_bin<Src, Walk64, 8, true>); else go(k_bin<Src, Walk64, 8, false>);
+                }
             } else if (k <= 16) {
-                if (w32) go(k_bin<Src, Walk32, 16>); else go(k_bin<Src, Walk64, 16>);
+                if (w32) go(k_bin<Src, Walk32, 16, false>); else go(k_bin<Src, Walk64, 16, false>);
             } else {
-                if (w32) go(k_bin<Src, Walk32, 32>); else go(k_bin<Src, Walk64, 32>);
+                if (w32) go(k_bin<Src, Walk32, 32, false>); else go(k_bin<Src, Walk64, 32, false>);
             }
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;

@@ -59,24 +59,28 @@ struct Mod32 {
 };
 
 // k positions of one key, i = 0, 1, ..., for d <= 2^31 (all sums fit 32 bits).
+// Position i+1 = (pos_i + h2 - c*2^64) mod d, where c = 1 when the wrapping
+// u64 sum h1 + i*h2 (src/bloom/mod.rs:194) carries out; so the two possible
+// increments, h2 mod d and (h2 - 2^64) mod d, are reduced once per key and
+// each step is a 64-bit add with carry, a select, an add and one conditional
+// subtract.
 struct Walk32 {
     uint64_t x, h2;
-    uint32_t r, s;
+    uint32_t r, s0, s1, d;
 
-    LSMB_HD Walk32(const Mod32& md, uint64_t h1, uint64_t h2_) : x(h1), h2(h2_) {
+    LSMB_HD Walk32(const Mod32& md, uint64_t h1, uint64_t h2_) : x(h1), h2(h2_), d(md.d) {
         r = md.reduce(h1);
-        s = md.reduce(h2_);
+        s0 = md.reduce(h2_);
+        const uint32_t t = s0 + md.dt;  // < 2d <= 2^32
+        s1 = t - md.d < t ? t - md.d : t;
     }
     LSMB_HD uint32_t pos() const { return r; }
-    LSMB_HD void next(const Mod32& md) {
+    LSMB_HD void next(const Mod32&) {
         uint64_t nx;
         const bool carry = __builtin_add_overflow(x, h2, &nx);
         x = nx;
-        uint32_t u = r + s;
-        u = u - md.d < u ? u - md.d : u;           // (r + s) mod d
-        uint32_t w = u + md.dt;
-        w = w - md.d < w ? w - md.d : w;           // (u - 2^64 mod d) mod d
-        r = carry ? w : u;
+        const uint32_t u = r + (carry ? s1 : s0);  // < 2d
+        r = u - d < u ? u - d : u;
     }
 };
 
