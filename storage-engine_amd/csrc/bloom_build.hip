@@ -84,331 +84,202 @@ __global__ __launch_bounds__(256) void k_build_atomic(Src src, uint64_t n, Mod32
 struct PassA {
     uint32_t b0, nb;        // this sweep's slices [b0, b0 + nb)
     uint32_t grid, cap;     // regions per slice, region capacity (segments)
+    uint32_t ring;          // ring entries per slice (multiple of 4, >= kSegEntries)
     uint64_t* regions;      // [nbins][grid][cap][8] u64
     uint32_t* counts;       // [nbins][grid] segments written
-    uint32_t* gw;           // filter words (overflow fallback only)
-    uint32_t* err;          // device error word: nonzero = a waiting loop hit LSMB_SPIN_LIMIT (a bug)
+    uint32_t* gw;           // filter words (ring / region overflow only)
+    uint32_t* err;          // device counters (LSMB_STATS builds)
 };
 
 __device__ __forceinline__ uint64_t* region_ptr(const PassA& a, uint32_t b, uint32_t w) {
     return a.regions + ((uint64_t)b * a.grid + w) * a.cap * kSegWords;
 }
 
-// LDS accessors through address_space(3) pointers, so every access in the
-// protocol is a DS instruction (a wave's DS operations execute in issue
-// order); a plain generic pointer would compile to FLAT accesses.
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
-typedef __attribute__((address_space(3))) uint64_t lds_u64;
-typedef __attribute__((address_space(3))) u32x4 lds_v4;
-
-// Orders this wave's earlier LDS writes before its later LDS atomics as seen
-// by other waves (s_waitcnt lgkmcnt(0)); also a compiler barrier.
-__device__ __forceinline__ void lds_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); }
-__device__ __forceinline__ void lds_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup"); }
-
 __device__ __forceinline__ void or_pos_global(uint32_t* gw, uint32_t b, uint32_t off) {
     const uint32_t p = (b << kSliceLog2) | off;
     atomicOr(gw + (p >> 5), 1u << (p & 31));
 }
 
-// Writes one packed segment (8 words, 24 offsets) as segment `seg` of region (b, w).
-__device__ __forceinline__ void write_segment(const PassA& a, const uint64_t* words, uint32_t b, uint32_t w,
-                                              uint32_t seg) {
-    uint64_t* dst = region_ptr(a, b, w) + (uint64_t)seg * kSegWords;
-    for (int j = 0; j < kSegWords; j++) dst[j] = words[j];
-}
-
-// Pass A LDS state, per slice of the sweep (136 B):
-//   half[lb][2][8]  u64  a ring of two 24-offset segments; entry e of a
-//                        segment is bits [20*(e>>3), +20) of word e&7
-//   state[lb]       u32  [gen1:8 | gen0:8 | claims:16]
-//   done[lb]        u32  [done1:16 | done0:16]
-// plus a 64-entry flush queue per wave.
-// Claim c (0, 1, 2, ...) is entry c%24 of segment s = c/24, which lives in
-// half s&1 and is written as segment s of the workgroup's region; gen_h counts
-// the segments half h has flushed, so the half is free for s exactly when
-// gen_{s&1} == s/2.  A lane claims with ONE ds_add_rtn on state, whose return
-// value is an atomic snapshot of (claims, gen0, gen1):
-//   - half free: OR the offset into it, then count it in done_h (the lane that
-//     brings done_h to 24 queues the segment's flush);
-//   - half still holding segment s-2 (rare): the lane keeps the claim in a
-//     small per-lane deferred list and completes it (OR + done) in a later
-//     iteration, once gen_h shows the half flushed;
-//   - region full (c >= cap*24; adversarial inputs): the claim is undone (the
-//     counter stays bounded) and the bit is set with a global atomic (exact:
-//     pass B reads the filter words after pass A).
-// Queued flushes run at the end of each key iteration, wave-cooperatively;
-// meanwhile the other half takes the slice's new claims.
-// Progress: an immediate claim's OR and done-count follow its claim within
-// the same iteration with no waiting; a deferred claim for segment s waits
-// only for segment s-2's flush, whose claims are immediate or deferred on
-// s-4, and so on down to a segment with only immediate claims.  Every loop
-// that waits (deferred list full, final drain) retries the wave's deferred
-// claims AND flushes its queue on each pass, and exits wave-uniformly
-// (ballot), so no lane ever holds back the work another lane waits for.
-// cap <= kMaxRegionSegs keeps claims < 2^16 and gens < 2^8.
-constexpr int kDefer = 2;       // deferred claims a lane can hold across iterations
-constexpr uint32_t kQueue = 64;  // per-wave flush queue entries
-
-struct BinLds {
-    uint64_t* half;
-    uint32_t* state;
-    uint32_t* done;
-    uint32_t* jq;  // this wave's flush queue: slice*2 + half
-};
-
-// Entry c of its slice: (word index within the slice's 16-word ring, bit shift).
-__device__ __forceinline__ void entry_slot(uint32_t c, uint32_t& word, uint32_t& sh) {
-    const uint32_t sg = c / (uint32_t)kSegEntries, e = c - sg * (uint32_t)kSegEntries;
-    word = ((sg & 1) << 3) | (e & 7);
-    sh = (e >> 3) * 20;
-}
-
-// Flushes the wave's queued segments, 16 per round: lane 4j+p copies piece p
-// (16 B) of job j to the region and zeroes it; then lane j releases job j's
-// half (done_h -= 24, gen_h += 1).  A store instruction costs the same
-// whatever its active lanes, hence the cooperation.
-__device__ __forceinline__ void flush_queue(const PassA& a, const BinLds& L, uint32_t w, uint32_t lane, uint32_t& qn) {
-    for (uint32_t r = 0; r < qn; r += 16) {
-        const uint32_t nj = min(16u, qn - r);
-        const uint32_t j = lane >> 2, piece = lane & 3;
-        if (j < nj) {
-            const uint32_t JJ = *(volatile lds_u32*)(lds_u32*)(L.jq + r + j);
-            const uint32_t JL = JJ >> 1, JH = JJ & 1;
-            const uint32_t g = (*(volatile lds_u32*)(lds_u32*)(L.state + JL) >> (16 + 8 * JH)) & 0xFFu;
-            const uint32_t sg = 2 * g + JH;  // < cap: claims past the region's capacity are undone
-            volatile lds_v4* hp = (volatile lds_v4*)(lds_u64*)(L.half + JL * 16 + JH * 8 + 2 * piece);
-            const u32x4 v = *hp;
-            *hp = u32x4{0, 0, 0, 0};
-            uint4* dst = reinterpret_cast<uint4*>(region_ptr(a, a.b0 + JL, w) + (uint64_t)sg * kSegWords) + piece;
-            *dst = make_uint4(v.x, v.y, v.z, v.w);
-        }
-        lds_release();
-        if (lane < nj) {
-            const uint32_t JJ = *(volatile lds_u32*)(lds_u32*)(L.jq + r + lane);
-            const uint32_t S = JJ >> 1, H = JJ & 1;
-            atomicSub(L.done + S, (uint32_t)kSegEntries << (16 * H));
-            lds_release();
-            atomicAdd(L.state + S, 1u << (16 + 8 * H));
-        }
-#ifdef LSMB_STATS
-        if (lane == 0) atomicAdd(a.err + 12, 1u);
-#endif
-    }
-    qn = 0;
-}
-
-// Appends the lanes' jobs (has) to the wave's queue (flushing first if full).
-__device__ __forceinline__ void queue_job(const PassA& a, const BinLds& L, uint32_t w, uint32_t lane, uint32_t& qn,
-                                          bool has, uint32_t J) {
-    const uint64_t bal = __ballot(has);
-    if (bal == 0) return;
-    const uint32_t cnt = (uint32_t)__popcll(bal);
-    if (qn + cnt > kQueue) flush_queue(a, L, w, lane, qn);
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-    if (has) *(volatile lds_u32*)(lds_u32*)(L.jq + qn + rank) = J;
-    qn += cnt;
-}
-
-// Completes the lane's deferred claims whose half has been flushed since and
-// queues the flushes they trigger.
-__device__ __forceinline__ void retry_deferred(const PassA& a, const BinLds& L, uint32_t w, uint32_t lane, uint32_t& qn,
-                                               const uint32_t (&dkey)[kDefer], const uint32_t (&doff)[kDefer],
-                                               uint32_t& dmask) {
-    uint32_t ready = 0;
-    if (dmask) {
-#pragma unroll
-        for (int d = 0; d < kDefer; d++) {
-            if (dmask >> d & 1) {
-                const uint32_t lb = dkey[d] >> 16, c = dkey[d] & 0xFFFFu;
-                const uint32_t sg = c / (uint32_t)kSegEntries, hh = sg & 1;
-                const uint32_t g = (*(volatile lds_u32*)(lds_u32*)(L.state + lb) >> (16 + 8 * hh)) & 0xFFu;
-                if (g == ((sg >> 1) & 0xFFu)) {
-                    uint32_t word, sh;
-                    entry_slot(c, word, sh);
-                    atomicOr(L.half + lb * 16 + word, (uint64_t)doff[d] << sh);
-                    ready |= 1u << d;
-                }
-            }
-        }
-    }
-    if (!__ballot(ready != 0)) return;
-    lds_release();
-    uint32_t dn[kDefer];
-#pragma unroll
-    for (int d = 0; d < kDefer; d++)
-        if (ready >> d & 1)
-            dn[d] = atomicAdd(L.done + (dkey[d] >> 16), 1u << (16 * (((dkey[d] & 0xFFFFu) / (uint32_t)kSegEntries) & 1)));
-    lds_acquire();
-#pragma unroll
-    for (int d = 0; d < kDefer; d++) {
-        const uint32_t hh = ((dkey[d] & 0xFFFFu) / (uint32_t)kSegEntries) & 1;
-        const bool job = (ready >> d & 1) && ((dn[d] >> (16 * hh)) & 0xFFFFu) == (uint32_t)kSegEntries - 1;
-        queue_job(a, L, w, lane, qn, job, (dkey[d] >> 16) * 2 + hh);
-    }
-    dmask &= ~ready;
-}
-
-// Passes a waiting loop may make before pass A reports an internal error
-// (LSMB_EHIP) instead of hanging: never reached unless the protocol is broken.
-#ifndef LSMB_SPIN_LIMIT
-#define LSMB_SPIN_LIMIT (1u << 24)
-#endif
-
-// Pass A.  One key per lane per iteration; W = Walk32 when num_bits <= 2^31,
-// else Walk64.  KMAX bounds k.  FULL: this sweep covers every slice (no
-// per-position sweep check).
+// Pass A (k_bin): hash keys, bin every position's 20-bit in-slice offset by
+// slice, write the bins to HBM as 64-B segments of packed offsets.
+//
+// One 1024-thread workgroup per CU owns a contiguous key range and walks it in
+// phases of one key per lane.  LDS holds, per slice of the sweep, a ring of
+// R u32 offsets plus its fill (bytes used) and the number of segments already
+// written to the workgroup's region for that slice:
+//   claim   one ds_add_rtn of 4 on the fill returns the entry's byte offset;
+//           the offset is stored with one ds_write_b32.  A claim past the ring
+//           (adversarial duplicates only; rare at the planned R) sets its bit
+//           with a global atomicOr instead: pass B reads the filter words
+//           after pass A, so the result is the same;
+//   barrier
+//   flush   wave v owns slices [v*SPW, (v+1)*SPW), one lane each.  Every full
+//           24-entry segment of an owned ring becomes a job; jobs are packed
+//           wave-cooperatively (4 lanes x 16 B per segment, 3 offsets per u64:
+//           entry e at bits 20*(e>>3) of word e&7) and stored to the region.
+//           The owner then moves the ring's remainder (< 24 entries) to the
+//           front and resets the fill;
+//   barrier
+// The next key's load is issued two phases ahead and its hash is computed
+// while this phase's claims are in flight, so VALU and LDS work overlap.
+// The protocol has no waiting loops and no global atomics on the hot path.
 template <class Src, class W, int KMAX, bool FULL>
 __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md, uint32_t k, PassA a) {
-    extern __shared__ uint64_t smem64[];
-    BinLds L;
-    L.half = smem64;                                    // nb * 16
-    L.state = (uint32_t*)(L.half + (size_t)a.nb * 16);  // nb
-    L.done = L.state + a.nb;                            // nb
-    const uint32_t tid = threadIdx.x, w = blockIdx.x, lane = tid & 63;
-    L.jq = L.done + a.nb + (tid >> 6) * kQueue;
-    const uint32_t climit = a.cap * (uint32_t)kSegEntries;
-    {
-        uint32_t* z = reinterpret_cast<uint32_t*>(smem64);
-        for (uint32_t i = tid; i < a.nb * (kLdsBytesPerBin / 4); i += kBinBlock) z[i] = 0;
-    }
-    __syncthreads();
+    extern __shared__ uint32_t sm[];
+    const uint32_t R = a.ring, R4 = 4 * a.ring, nb = a.nb;
+    uint32_t* fill = sm + (size_t)nb * R;  // bytes used in each ring
+    uint32_t* segs = fill + nb;            // segments written to each region
+    const uint32_t tid = threadIdx.x, w = blockIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t* jobs = segs + nb + wave * kJobSlots;
+    for (uint32_t i = tid; i < 2 * nb; i += kBinBlock) fill[i] = 0;
 
-    uint32_t qn = 0;                                 // wave-uniform: queued flushes
-    uint32_t dkey[kDefer], doff[kDefer], dmask = 0;  // deferred claims: (slice << 16 | claim), offset
     // Workgroup w owns keys [w*per, (w+1)*per): a contiguous, coalesced run.
     const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
     const uint64_t i0 = (uint64_t)w * per, i1 = min(n, i0 + per);
-    // The loop is uniform across the workgroup (lanes past i1 just carry no
-    // positions): the cooperative flush needs every lane of the wave.
-    const uint64_t iters = i1 > i0 ? (i1 - i0 + kBinBlock - 1) / kBinBlock : 0;
-    for (uint64_t it = 0; it < iters; it++) {
-        const uint64_t i = i0 + it * kBinBlock + tid;
-        uint32_t lb[KMAX], off[KMAX], st[KMAX];
-        uint32_t pend = 0;
-        if (i < i1) {
-            const H128 h = src.hash(i);
+    const uint64_t iters = i1 > i0 ? (i1 - i0 + kBinBlock - 1) / kBinBlock : 0;  // uniform over the workgroup
+    const uint32_t spw = (nb + 15) / 16;  // slices per wave (<= 64)
+    const uint32_t own = wave * spw + lane;
+    const bool owner = lane < spw && own < nb;
+
+    // Positions of the key this lane claims in the current phase; ~0u = none.
+    uint32_t pos[KMAX];
+    auto positions = [&](const typename Src::Pre& pre, uint64_t i, bool ok, uint32_t (&out)[KMAX]) {
+#pragma unroll
+        for (int q = 0; q < KMAX; q++) out[q] = ~0u;
+        if (ok) {
+            const H128 h = src.hash_pre(pre, i);
             W walk(md, h.lo, h.hi);
 #pragma unroll
             for (int q = 0; q < KMAX; q++) {
                 if ((uint32_t)q < k) {
                     const uint32_t p = walk.pos();
-                    const uint32_t b = (p >> kSliceLog2) - (FULL ? 0u : a.b0);
-                    lb[q] = b;
-                    off[q] = p & kSliceMask;
-                    if (FULL || b < a.nb) pend |= 1u << q;
+                    if (FULL || (p >> kSliceLog2) - a.b0 < nb) out[q] = p;
                     walk.next(md);
                 }
             }
         }
-        // Claims, issued back to back (a result used inside its own `if`
-        // makes the compiler wait for each in turn).
-#pragma unroll
-        for (int q = 0; q < KMAX; q++)
-            if (pend >> q & 1) st[q] = atomicAdd(L.state + lb[q], 1u);
-        // Immediate claims: OR the offset in.  Others: region full -> undo +
-        // global atomic; half busy -> deferred.
-        uint32_t cmask = 0, dnew = 0;
+    };
+    auto key_index = [&](uint64_t it) { return i0 + it * kBinBlock + tid; };
+    typename Src::Pre pre0 = src.fetch(key_index(0), key_index(0) < i1);
+    typename Src::Pre pre1 = src.fetch(key_index(1), iters > 1 && key_index(1) < i1);
+    typename Src::Pre pre2 = src.fetch(key_index(2), iters > 2 && key_index(2) < i1);
+    positions(pre0, key_index(0), iters > 0 && key_index(0) < i1, pos);
+    __syncthreads();
+
+    for (uint64_t it = 0; it < iters; it++) {
+        // Claims for this phase's key, back to back.
+        uint32_t got[KMAX];
 #pragma unroll
         for (int q = 0; q < KMAX; q++) {
-            if (pend >> q & 1) {
-                const uint32_t c = st[q] & 0xFFFFu, sg = c / (uint32_t)kSegEntries, hh = sg & 1;
-                const uint32_t e = c - sg * (uint32_t)kSegEntries;
-                const bool free_half = ((st[q] >> (16 + 8 * hh)) & 0xFFu) == ((sg >> 1) & 0xFFu);
-                if (c >= climit) {
-                    atomicSub(L.state + lb[q], 1u);
-                    or_pos_global(a.gw, a.b0 + lb[q], off[q]);
-                } else if (free_half) {
-                    atomicOr(L.half + lb[q] * 16 + (hh << 3) + (e & 7), (uint64_t)off[q] << ((e >> 3) * 20));
-                    cmask |= 1u << q;
-                    st[q] = hh;  // from here on: the half
+            got[q] = ~0u;
+            if ((uint32_t)q < k && pos[q] != ~0u) {
+                const uint32_t b = (pos[q] >> kSliceLog2) - (FULL ? 0u : a.b0);
+                got[q] = atomicAdd(fill + b, 4u);
+            }
+        }
+        // Next phase's key: hash while the claims are in flight.
+        uint32_t npos[KMAX];
+        {
+            const uint64_t inext = key_index(it + 1);
+            positions(pre1, inext, it + 1 < iters && inext < i1, npos);
+            pre1 = pre2;
+            pre2 = src.fetch(key_index(it + 3), it + 3 < iters && key_index(it + 3) < i1);
+        }
+        // Store the claimed entries.
+#pragma unroll
+        for (int q = 0; q < KMAX; q++) {
+            if ((uint32_t)q < k && pos[q] != ~0u) {
+                const uint32_t b = (pos[q] >> kSliceLog2) - (FULL ? 0u : a.b0);
+                const uint32_t off = pos[q] & kSliceMask;
+                if (got[q] < R4) {
+                    *(uint32_t*)((char*)sm + (b * R4 + got[q])) = off;
                 } else {
-                    dnew |= 1u << q;
+                    or_pos_global(a.gw, a.b0 + b, off);
+#ifdef LSMB_STATS
+                    atomicAdd(a.err + 9, 1u);
+#endif
                 }
             }
         }
-        lds_release();
-        uint32_t dn[KMAX];
 #pragma unroll
-        for (int q = 0; q < KMAX; q++)
-            if (cmask >> q & 1) dn[q] = atomicAdd(L.done + lb[q], 1u << (16 * st[q]));
-        lds_acquire();
-#ifdef LSMB_STATS
-        if (dnew) atomicAdd(a.err + 9, (uint32_t)__popc(dnew));
-        if (lane == 0) atomicAdd(a.err + 11, 1u);
-#endif
-#pragma unroll
-        for (int q = 0; q < KMAX; q++) {
-            if ((uint32_t)q < k) {
-                const bool job = (cmask >> q & 1) && ((dn[q] >> (16 * st[q])) & 0xFFFFu) == (uint32_t)kSegEntries - 1;
-                queue_job(a, L, w, lane, qn, job, lb[q] * 2 + st[q]);
-            }
+        for (int q = 0; q < KMAX; q++) pos[q] = npos[q];
+        __syncthreads();
+
+        // Flush the owned slices' full segments.
+        uint32_t cnt = 0, nf = 0, sg0 = 0;
+        if (owner) {
+            cnt = min(fill[own], R4) >> 2;
+            nf = cnt / (uint32_t)kSegEntries;
+            sg0 = segs[own];
         }
-        // Older deferred claims (their halves may have been flushed since),
-        // then every queued flush.
-        retry_deferred(a, L, w, lane, qn, dkey, doff, dmask);
-        flush_queue(a, L, w, lane, qn);
-        // New deferred claims go to free list entries; while a lane has more
-        // than fit, the wave keeps completing deferred claims and flushing.
-        if (__ballot(dnew != 0)) {
-            for (uint32_t spin = 0;; spin++) {
+        for (uint32_t j = 0; __ballot(j < nf); j++) {
+            const bool has = j < nf;
+            const uint64_t bal = __ballot(has);
+            const uint32_t total = (uint32_t)__popcll(bal);
+            if (has) {
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                jobs[rank] = own | (j << 11) | ((sg0 + j) << 16);
+            }
+            for (uint32_t r = 0; r < total; r += 16) {
+                const uint32_t jj = r + (lane >> 2), piece = lane & 3;
+                if (jj < total) {
+                    const uint32_t J = jobs[jj];
+                    const uint32_t b = J & 2047u, rj = (J >> 11) & 31u, sg = J >> 16;
+                    const uint32_t* e = sm + b * R + rj * kSegEntries + 2 * piece;
+                    const uint2 x = *(const uint2*)e, y = *(const uint2*)(e + 8), z = *(const uint2*)(e + 16);
+                    const uint64_t w0 = (uint64_t)x.x | ((uint64_t)y.x << 20) | ((uint64_t)z.x << 40);
+                    const uint64_t w1 = (uint64_t)x.y | ((uint64_t)y.y << 20) | ((uint64_t)z.y << 40);
+                    if (sg < a.cap) {
+                        uint4* dst = reinterpret_cast<uint4*>(region_ptr(a, a.b0 + b, w) + (uint64_t)sg * kSegWords) + piece;
+                        *dst = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+                    } else {  // region full (adversarial inputs): exact global atomics
+                        const uint32_t vals[6] = {x.x, y.x, z.x, x.y, y.y, z.y};
 #pragma unroll
-                for (int q = 0; q < KMAX; q++) {
-                    if (dnew >> q & 1) {
-                        const int fr = __ffs(~dmask & ((1u << kDefer) - 1)) - 1;
-                        if (fr >= 0) {
-                            const uint32_t c = st[q] & 0xFFFFu;
-#pragma unroll
-                            for (int d = 0; d < kDefer; d++)
-                                if (d == fr) {
-                                    dkey[d] = (lb[q] << 16) | c;
-                                    doff[d] = off[q];
-                                }
-                            dmask |= 1u << fr;
-                            dnew &= ~(1u << q);
-                        }
+                        for (int t = 0; t < 6; t++) or_pos_global(a.gw, a.b0 + b, vals[t]);
+#ifdef LSMB_STATS
+                        atomicAdd(a.err + 7, 6u);
+#endif
                     }
                 }
-                if (!__ballot(dnew != 0)) break;
-                if (spin == LSMB_SPIN_LIMIT) {
-                    if (lane == 0) atomicOr(a.err, 2u);
-                    break;
-                }
-#ifdef LSMB_STATS
-                if (lane == 0) atomicAdd(a.err + 10, 1u);
-#endif
-                retry_deferred(a, L, w, lane, qn, dkey, doff, dmask);
-                flush_queue(a, L, w, lane, qn);
-                if (spin) __builtin_amdgcn_s_sleep(2);
             }
         }
-    }
-    // Drain: complete every deferred claim.
-    for (uint32_t spin = 0; __ballot(dmask != 0); spin++) {
-        if (spin == LSMB_SPIN_LIMIT) {
-            if (lane == 0) atomicOr(a.err, 4u);
-            break;
+        if (owner && nf) {
+            // Remainder to the front of the ring (source starts at entry >= 24,
+            // so it never overlaps the destination; reading up to 3 entries
+            // past the fill is harmless).
+            const uint32_t rem = cnt - nf * (uint32_t)kSegEntries;
+            const uint4* s4 = reinterpret_cast<const uint4*>(sm + own * R + nf * kSegEntries);
+            uint4* d4 = reinterpret_cast<uint4*>(sm + own * R);
+            for (uint32_t c = 0; c < rem; c += 4) d4[c >> 2] = s4[c >> 2];
+            fill[own] = rem * 4;
+            segs[own] = min(sg0 + nf, a.cap);  // keeps job words' 16-bit segment field exact
         }
-        retry_deferred(a, L, w, lane, qn, dkey, doff, dmask);
-        flush_queue(a, L, w, lane, qn);
-        if (spin) __builtin_amdgcn_s_sleep(2);
+        __syncthreads();
     }
-    __syncthreads();
-    // The open segment of each slice (claims % 24 entries), padded with
-    // copies of its first offset (setting a bit twice is a no-op), then the
-    // per-region segment counts.
-    for (uint32_t lb = tid; lb < a.nb; lb += kBinBlock) {
-        const uint32_t c = min(L.state[lb] & 0xFFFFu, climit);
-        const uint32_t sg = c / (uint32_t)kSegEntries, r = c % (uint32_t)kSegEntries;
-        if (r) {
-            uint64_t words[kSegWords];
-            const uint64_t* hp = L.half + lb * 16 + (sg & 1) * 8;
-            for (int j = 0; j < kSegWords; j++) words[j] = hp[j];
-            const uint64_t first = words[0] & kSliceMask;
-            for (uint32_t e = r; e < (uint32_t)kSegEntries; e++) words[e & 7] |= first << (20 * (e >> 3));
-            write_segment(a, words, a.b0 + lb, w, sg);
+
+    // The last open segment of each owned slice (fill < 24 entries), padded
+    // with copies of its first offset (setting a bit twice is a no-op), and
+    // the region's segment count.
+    if (owner) {
+        const uint32_t cnt = fill[own] >> 2;
+        uint32_t sg = segs[own];
+        if (cnt) {
+            const uint32_t* e = sm + own * R;
+            uint32_t v[kSegEntries];
+#pragma unroll
+            for (int t = 0; t < kSegEntries; t++) v[t] = (uint32_t)t < cnt ? e[t] : e[0];
+            if (sg < a.cap) {
+                uint64_t* dst = region_ptr(a, a.b0 + own, w) + (uint64_t)sg * kSegWords;
+#pragma unroll
+                for (int t = 0; t < kSegWords; t++)
+                    dst[t] = (uint64_t)v[t] | ((uint64_t)v[t + 8] << 20) | ((uint64_t)v[t + 16] << 40);
+            } else {
+                for (uint32_t t = 0; t < cnt; t++) or_pos_global(a.gw, a.b0 + own, v[t]);
+            }
+            sg++;
         }
-        a.counts[(uint64_t)(a.b0 + lb) * a.grid + w] = sg + (r ? 1u : 0u);
+        a.counts[(uint64_t)(a.b0 + own) * a.grid + w] = min(sg, a.cap);
     }
 }
 
@@ -523,11 +394,12 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
             a.nb = min(pl.bins_per_sweep, pl.nbins - a.b0);
             a.grid = pl.grid;
             a.cap = pl.cap_segs;
+            a.ring = pl.ring;
             a.regions = ws.regions;
             a.counts = ws.counts;
             a.gw = gw;
             a.err = ws.err;
-            const size_t smem = (size_t)a.nb * kLdsBytesPerBin + (kBinBlock / 64) * kQueue * 4;  // + flush queues
+            const size_t smem = (size_t)a.nb * (4 * a.ring + kBinExtraBytes) + (kBinBlock / 64) * kJobSlots * 4;
             auto go = [&](auto kern) {
                 hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
                 kern<<<dim3(pl.grid), dim3(kBinBlock), smem, st>>>(src, n, md, k, a);
@@ -586,15 +458,29 @@ BuildStrategy pick_build_strategy(uint32_t num_bits, uint32_t k, uint64_t n) {
 PartitionPlan plan_partition(uint32_t num_bits, uint32_t k, uint64_t n, int num_cus) {
     PartitionPlan pl;
     pl.nbins = (uint32_t)(((uint64_t)num_bits + kSliceMask) >> kSliceLog2);
-    // <= kMaxBinsPerSweep slices per sweep keep a pass A workgroup within its
-    // LDS (one 1024-thread workgroup per CU); bigger filters take more sweeps
-    // (each re-reads and re-hashes the keys, and keeps only its slices).
+    // Entries a slice's ring receives per pass A phase (1024 keys), and the
+    // ring that holds a segment's worth of leftovers plus a phase's arrivals
+    // with margin.  Claims past the ring fall back to exact global atomics.
+    const double lambda = (double)kBinBlock * k * fmin(1.0, (double)(1u << kSliceLog2) / (double)num_bits);
+    uint32_t need = kSegEntries + (uint32_t)ceil(lambda + 2.0 * sqrt(lambda));
+    need = (need + 3) & ~3u;
+    if (need > kMaxRing) need = kMaxRing & ~3u;
+    // Fewest sweeps whose slices fit LDS with that ring; each sweep re-reads
+    // and re-hashes the keys and keeps only its own slices' positions.
     pl.sweeps = (pl.nbins + kMaxBinsPerSweep - 1) / kMaxBinsPerSweep;
-    pl.bins_per_sweep = (pl.nbins + pl.sweeps - 1) / pl.sweeps;
-    const uint32_t per_cu = pl.bins_per_sweep * kLdsBytesPerBin <= 80 * 1024 ? 2 : 1;
-    // at least ~kBinBlock keys per workgroup
+    for (;; pl.sweeps++) {
+        pl.bins_per_sweep = (pl.nbins + pl.sweeps - 1) / pl.sweeps;
+        uint32_t r = (kBinLdsBudget / pl.bins_per_sweep - kBinExtraBytes) / 4;
+        r &= ~3u;
+        if (r > kMaxRing) r = kMaxRing & ~3u;
+        if (r >= need || pl.bins_per_sweep == 1) {
+            pl.ring = r;
+            break;
+        }
+    }
+    // one 1024-thread workgroup per CU, at least ~kBinBlock keys each
     const uint64_t gmax = (n + kBinBlock - 1) / kBinBlock;
-    uint64_t g = (uint64_t)num_cus * per_cu;
+    uint64_t g = (uint64_t)num_cus;
     if (g > gmax) g = gmax;
     if (g < 1) g = 1;
     pl.grid = (uint32_t)g;
@@ -604,7 +490,7 @@ PartitionPlan plan_partition(uint32_t num_bits, uint32_t k, uint64_t n, int num_
     const double mu = (double)keys_w * k * p;
     const double cap_e = mu + 8.0 * sqrt(mu) + 2.0 * kSegEntries;
     pl.cap_segs = (uint32_t)ceil(cap_e / kSegEntries);
-    // A region holds at most kMaxRegionSegs segments (pass A's state word);
+    // A region holds at most kMaxRegionSegs segments (pass A's job word);
     // a bigger plan is reported as unbounded so callers chunk the keys.
     pl.region_bytes = pl.cap_segs > kMaxRegionSegs ? ~0ull >> 2 : (uint64_t)pl.nbins * pl.grid * pl.cap_segs * 64;
     pl.counts_bytes = (uint64_t)pl.nbins * pl.grid * 4;

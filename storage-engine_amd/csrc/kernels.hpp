@@ -17,9 +17,13 @@ constexpr int kSegWords = 8;                          // 3 offsets per u64 word
 constexpr int kBinBlock = 1024;                       // pass A workgroup
 constexpr int kApplyBlock = 1024;                     // pass B workgroup
 constexpr uint32_t kLdsFilterMaxWords32 = 40 * 1024;  // 160 KiB: whole filter in LDS
-constexpr uint32_t kLdsBytesPerBin = 2 * kSegWords * 8 + 4 + 4;  // two packed segments + state + done
-constexpr uint32_t kMaxBinsPerSweep = 1152;                // <= 153 KiB of pass A LDS (+ 4 KiB flush queues)
-constexpr uint32_t kMaxRegionSegs = 510;                  // pass A state: claims < 2^16, gens < 2^8
+constexpr uint32_t kLdsBytes = 160 * 1024;            // LDS per CU (gfx950)
+constexpr uint32_t kJobSlots = 64;                    // pass A: per-wave flush job list (u32 each)
+constexpr uint32_t kBinLdsBudget = kLdsBytes - (kBinBlock / 64) * kJobSlots * 4;  // rings + per-slice words
+constexpr uint32_t kBinExtraBytes = 8;                // per slice besides its ring: fill + segments written
+constexpr uint32_t kMaxBinsPerSweep = 1024;           // one owner lane per slice: <= 64 slices per wave
+constexpr uint32_t kMaxRing = 31 * kSegEntries;       // ring entries per slice (job word: 5-bit ring segment)
+constexpr uint32_t kMaxRegionSegs = 65000;            // job word: 16-bit region segment index (+ ring segments)
 
 // How a key batch is presented to the kernels.
 struct KeyBatch {
@@ -43,6 +47,7 @@ struct PartitionPlan {
     uint32_t grid = 0;            // pass A workgroups = regions per slice
     uint32_t cap_segs = 0;        // region capacity, segments
     uint32_t bins_per_sweep = 0;  // slices buffered in LDS per pass A launch
+    uint32_t ring = 0;            // pass A ring entries per slice (multiple of 4, >= kSegEntries)
     uint32_t sweeps = 0;
     uint64_t region_bytes = 0;    // nbins * grid * cap_segs * 64
     uint64_t counts_bytes = 0;    // nbins * grid * 4

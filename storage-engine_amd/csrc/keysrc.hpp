@@ -25,6 +25,14 @@ struct Fixed16 {
     }
     __device__ __forceinline__ const uint8_t* bytes(uint64_t i) const { return reinterpret_cast<const uint8_t*>(k + i); }
     __device__ __forceinline__ uint64_t key_len(uint64_t) const { return 16; }
+    // Split load / hash, so a kernel can issue key i's load iterations ahead.
+    using Pre = uint4;
+    __device__ __forceinline__ Pre fetch(uint64_t i, bool ok) const {
+        return ok ? ld_stream16(k + i) : make_uint4(0, 0, 0, 0);
+    }
+    __device__ __forceinline__ H128 hash_pre(const Pre& v, uint64_t) const {
+        return xxh3_16(((uint64_t)v.y << 32) | v.x, ((uint64_t)v.w << 32) | v.z);
+    }
 };
 
 // Any fixed key length, any alignment.
@@ -34,6 +42,9 @@ struct FixedN {
     __device__ __forceinline__ H128 hash(uint64_t i) const { return xxh3_128(d + i * len, len); }
     __device__ __forceinline__ const uint8_t* bytes(uint64_t i) const { return d + i * len; }
     __device__ __forceinline__ uint64_t key_len(uint64_t) const { return len; }
+    struct Pre {};
+    __device__ __forceinline__ Pre fetch(uint64_t, bool) const { return Pre{}; }
+    __device__ __forceinline__ H128 hash_pre(const Pre&, uint64_t i) const { return hash(i); }
 };
 
 // Packed variable-length keys: key i = d[o[i] .. o[i+1]).
@@ -46,6 +57,12 @@ struct VarLen {
     }
     __device__ __forceinline__ const uint8_t* bytes(uint64_t i) const { return d + o[i]; }
     __device__ __forceinline__ uint64_t key_len(uint64_t i) const { return o[i + 1] - o[i]; }
+    // The offset pair is fetched ahead; the key bytes are read by the hash.
+    struct Pre {
+        uint64_t a, b;
+    };
+    __device__ __forceinline__ Pre fetch(uint64_t i, bool ok) const { return ok ? Pre{o[i], o[i + 1]} : Pre{0, 0}; }
+    __device__ __forceinline__ H128 hash_pre(const Pre& p, uint64_t) const { return xxh3_128(d + p.a, p.b - p.a); }
 };
 
 }  // namespace ks

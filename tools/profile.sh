@@ -8,7 +8,7 @@ REPO=${GRAFT_REPO_ROOT:-/root/repo}
 OUT=$REPO/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-BENCH="$REPO/bench.py --steps 10 --warmup 2 --no-cpu-baseline $*"
+BENCH="$REPO/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e $*"
 run() {  # name, rocprofv3 args...
   local name=$1; shift
   timeout -k 10 300 rocprofv3 "$@" --output-format csv -d "$OUT/$name" -o run -- python3 $BENCH > "$OUT/$name.log" 2>&1
