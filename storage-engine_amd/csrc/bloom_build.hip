@@ -30,6 +30,12 @@
 #include "kernels.hpp"
 #include "keysrc.hpp"
 
+// LSMB_ABL (timing ablations for tools/, never in the product build):
+//   1 = no segment flush, 2 = no claims/stores, 8 = no region stores.
+#ifndef LSMB_ABL
+#define LSMB_ABL 0
+#endif
+
 namespace lsmb {
 namespace {
 
@@ -84,15 +90,25 @@ __global__ __launch_bounds__(256) void k_build_atomic(Src src, uint64_t n, Mod32
 struct PassA {
     uint32_t b0, nb;        // this sweep's slices [b0, b0 + nb)
     uint32_t grid, cap;     // regions per slice, region capacity (segments)
-    uint32_t ring;          // ring entries per slice (multiple of 4, >= kSegEntries)
+    uint32_t ring;          // ring entries per slice (multiple of 8, >= kSegEntries)
     uint64_t* regions;      // [nbins][grid][cap][8] u64
     uint32_t* counts;       // [nbins][grid] segments written
     uint32_t* gw;           // filter words (ring / region overflow only)
     uint32_t* err;          // device counters (LSMB_STATS builds)
+    uint64_t* dummy;        // [grid][kBinBlock][4] u64: stores of lanes without a flush job
 };
 
 __device__ __forceinline__ uint64_t* region_ptr(const PassA& a, uint32_t b, uint32_t w) {
     return a.regions + ((uint64_t)b * a.grid + w) * a.cap * kSegWords;
+}
+
+// Workgroup barrier that waits for this wave's LDS operations only.
+// __syncthreads() also drains vmcnt, i.e. waits for every outstanding global
+// store and prefetch load; pass A's region stores and next-key loads are
+// consumed by no other wave of this launch, so they stay in flight across
+// phases.  The store data leaves the VGPRs at issue.
+__device__ __forceinline__ void lds_barrier() {
+    __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 __device__ __forceinline__ void or_pos_global(uint32_t* gw, uint32_t b, uint32_t off) {
@@ -100,38 +116,56 @@ __device__ __forceinline__ void or_pos_global(uint32_t* gw, uint32_t b, uint32_t
     atomicOr(gw + (p >> 5), 1u << (p & 31));
 }
 
+__device__ __forceinline__ uint64_t pack3(uint32_t x, uint32_t y, uint32_t z) {
+    return (uint64_t)x | ((uint64_t)y << 20) | ((uint64_t)z << 40);
+}
+
 // Pass A (k_bin): hash keys, bin every position's 20-bit in-slice offset by
 // slice, write the bins to HBM as 64-B segments of packed offsets.
 //
 // One 1024-thread workgroup per CU owns a contiguous key range and walks it in
-// phases of one key per lane.  LDS holds, per slice of the sweep, a ring of
-// R u32 offsets plus its fill (bytes used) and the number of segments already
-// written to the workgroup's region for that slice:
-//   claim   one ds_add_rtn of 4 on the fill returns the entry's byte offset;
-//           the offset is stored with one ds_write_b32.  A claim past the ring
-//           (adversarial duplicates only; rare at the planned R) sets its bit
-//           with a global atomicOr instead: pass B reads the filter words
-//           after pass A, so the result is the same;
+// phases of one key per lane.  LDS holds, per slice of the sweep, a ring of R
+// u32 offsets (R a multiple of 8) and a fill word
+//     lo16 = ring start + 4 * claims (bytes, unwrapped), hi16 = claims,
+// plus one sink slice (index nb) that absorbs the claims of lanes with no
+// position (tail keys, positions outside the sweep) with an increment of 0.
+//   claim   one ds_add_rtn of (4 | 1 << 16) returns the entry's slot; the
+//           offset is stored with one ds_write_b32 (branch-free).  A claim
+//           past the ring (adversarial duplicates only; rare at the planned R)
+//           stores into the sink and sets its bit with a global atomicOr:
+//           pass B reads the filter words after pass A, so the result is exact;
 //   barrier
-//   flush   wave v owns slices [v*SPW, (v+1)*SPW), one lane each.  Every full
-//           24-entry segment of an owned ring becomes a job; jobs are packed
-//           wave-cooperatively (4 lanes x 16 B per segment, 3 offsets per u64:
-//           entry e at bits 20*(e>>3) of word e&7) and stored to the region.
-//           The owner then moves the ring's remainder (< 24 entries) to the
-//           front and resets the fill;
+//   flush   wave v owns slices [v*SPW, (v+1)*SPW), one lane each, which keeps
+//           its ring's start and its region's segment count in registers.
+//           Every full 24-entry segment becomes a job; two lanes per job read
+//           its three 8-entry groups (ds_read_b128; 8 | R, so a group never
+//           wraps), pack 3 offsets per u64 (entry e at bits 20*(e>>3) of word
+//           e&7) and store 32 B each to the region.  The owner advances the
+//           start and rewrites the fill word;
 //   barrier
 // The next key's load is issued two phases ahead and its hash is computed
-// while this phase's claims are in flight, so VALU and LDS work overlap.
-// The protocol has no waiting loops and no global atomics on the hot path.
-template <class Src, class W, int KMAX, bool FULL>
-__global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md, uint32_t k, PassA a) {
+// while this phase's claims are in flight.  No waiting loops, no global
+// atomics on the hot path.  EXACT: k == KMAX at compile time (k = 7 is what
+// BloomFilter::new yields for fpr = 0.01).
+constexpr uint32_t kAhead = 4;  // pass A key prefetch distance, in phases
+
+template <class Src, class W, int KMAX, bool EXACT, bool FULL>
+__global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md, uint32_t k_, PassA a) {
     extern __shared__ uint32_t sm[];
+    const uint32_t k = EXACT ? (uint32_t)KMAX : k_;
     const uint32_t R = a.ring, R4 = 4 * a.ring, nb = a.nb;
-    uint32_t* fill = sm + (size_t)nb * R;  // bytes used in each ring
-    uint32_t* segs = fill + nb;            // segments written to each region
+    uint32_t* fill = sm + (size_t)(nb + 1) * R;  // nb + 1 fill words (the last: sink)
     const uint32_t tid = threadIdx.x, w = blockIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint32_t* jobs = segs + nb + wave * kJobSlots;
-    for (uint32_t i = tid; i < 2 * nb; i += kBinBlock) fill[i] = 0;
+    uint32_t* jobs = fill + nb + 1 + wave * kJobSlots;
+    for (uint32_t i = tid; i <= nb; i += kBinBlock) fill[i] = 0;
+    for (uint32_t i = tid; i < (kBinBlock / 64) * kJobSlots; i += kBinBlock) fill[nb + 1 + i] = 0;
+    constexpr uint32_t kInc = 4u | (1u << 16);
+    const uint32_t sink = nb << kSliceLog2;  // local position of the sink slice
+    const uint32_t lim = R << 16;            // fill < lim <=> claims < R
+    // Where lanes without a flush job store (keeps the store count static):
+    // 32 B per thread, so the stores never contend for one address and stay
+    // in L2 (plain stores, rewritten every phase).
+    uint4* const dummy = reinterpret_cast<uint4*>(a.dummy) + ((uint64_t)w * kBinBlock + tid) * 2;
 
     // Workgroup w owns keys [w*per, (w+1)*per): a contiguous, coalesced run.
     const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
@@ -140,146 +174,201 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
     const uint32_t spw = (nb + 15) / 16;  // slices per wave (<= 64)
     const uint32_t own = wave * spw + lane;
     const bool owner = lane < spw && own < nb;
+    uint32_t start = 0, segs = 0;  // owner: ring start (bytes), region segments written
 
-    // Positions of the key this lane claims in the current phase; ~0u = none.
-    uint32_t pos[KMAX];
-    auto positions = [&](const typename Src::Pre& pre, uint64_t i, bool ok, uint32_t (&out)[KMAX]) {
+    // Local positions (p - b0 * 2^20) of the key this lane claims in the
+    // current phase; `sink` where there is none.  kinc: this key's increment.
+    uint32_t pos[KMAX], kinc = 0;
+    auto walk_positions = [&](const H128& h, bool ok, uint32_t (&out)[KMAX]) {
+        W walk(md, h.lo, h.hi);
 #pragma unroll
-        for (int q = 0; q < KMAX; q++) out[q] = ~0u;
-        if (ok) {
-            const H128 h = src.hash_pre(pre, i);
-            W walk(md, h.lo, h.hi);
-#pragma unroll
-            for (int q = 0; q < KMAX; q++) {
-                if ((uint32_t)q < k) {
-                    const uint32_t p = walk.pos();
-                    if (FULL || (p >> kSliceLog2) - a.b0 < nb) out[q] = p;
-                    walk.next(md);
-                }
+        for (int q = 0; q < KMAX; q++) {
+            if (EXACT || (uint32_t)q < k) {
+                const uint32_t lp = walk.pos() - (FULL ? 0u : (a.b0 << kSliceLog2));
+                out[q] = ok && (FULL || lp < sink) ? lp : sink;
+                if (q + 1 < KMAX) walk.next(md);
             }
         }
     };
     auto key_index = [&](uint64_t it) { return i0 + it * kBinBlock + tid; };
-    typename Src::Pre pre0 = src.fetch(key_index(0), key_index(0) < i1);
-    typename Src::Pre pre1 = src.fetch(key_index(1), iters > 1 && key_index(1) < i1);
-    typename Src::Pre pre2 = src.fetch(key_index(2), iters > 2 && key_index(2) < i1);
-    positions(pre0, key_index(0), iters > 0 && key_index(0) < i1, pos);
+    auto key_ok = [&](uint64_t it) { return it < iters && key_index(it) < i1; };
+    // Keys are loaded kAhead phases before they are hashed, into kAhead
+    // buffers with static roles (the loop is unrolled kAhead times, so no
+    // register copy forces a vmcnt drain).  gfx9 retires loads and stores in
+    // one in-order vmcnt queue: a key load completes only after every older
+    // region store, so the distance must cover the store round trip too.
+    typename Src::Pre pb0, pb1, pb2, pb3;  // key m lives in pb[m % 4]
+    {
+        const bool ok = key_ok(0);
+        const typename Src::Pre p = src.fetch(key_index(0), ok);
+        const H128 h = ok ? src.hash_pre(p, key_index(0)) : H128{0, 0};
+        walk_positions(h, ok, pos);
+        kinc = ok ? kInc : 0u;
+    }
+    pb1 = src.fetch(key_index(1), key_ok(1));
+    pb2 = src.fetch(key_index(2), key_ok(2));
+    pb3 = src.fetch(key_index(3), key_ok(3));
+    pb0 = src.fetch(key_index(4), key_ok(4));
     __syncthreads();
 
-    for (uint64_t it = 0; it < iters; it++) {
+    // One phase: claim key it's positions, hash key it+1 (from `pre`) and
+    // reload `pre` with key it+1+kAhead, store the entries, flush.
+    auto phase = [&](uint64_t it, typename Src::Pre& pre) __attribute__((always_inline)) {
         // Claims for this phase's key, back to back.
         uint32_t got[KMAX];
 #pragma unroll
         for (int q = 0; q < KMAX; q++) {
-            got[q] = ~0u;
-            if ((uint32_t)q < k && pos[q] != ~0u) {
-                const uint32_t b = (pos[q] >> kSliceLog2) - (FULL ? 0u : a.b0);
-                got[q] = atomicAdd(fill + b, 4u);
+            if (EXACT || (uint32_t)q < k) {
+                const uint32_t inc = FULL ? kinc : (pos[q] < sink ? kInc : 0u);
+                got[q] = (LSMB_ABL & 2) ? pos[q] : atomicAdd(fill + (pos[q] >> kSliceLog2), inc);
             }
         }
         // Next phase's key: hash while the claims are in flight.
-        uint32_t npos[KMAX];
-        {
-            const uint64_t inext = key_index(it + 1);
-            positions(pre1, inext, it + 1 < iters && inext < i1, npos);
-            pre1 = pre2;
-            pre2 = src.fetch(key_index(it + 3), it + 3 < iters && key_index(it + 3) < i1);
-        }
-        // Store the claimed entries.
+        const bool nok = key_ok(it + 1);
+        const H128 nh = src.hash_pre(pre, key_index(it + 1));
+        pre = src.fetch(key_index(it + 1 + kAhead), key_ok(it + 1 + kAhead));
+        // Store the claimed entries (overflowing claims into the sink's slot 0).
+        uint32_t gmax = 0;
 #pragma unroll
         for (int q = 0; q < KMAX; q++) {
-            if ((uint32_t)q < k && pos[q] != ~0u) {
-                const uint32_t b = (pos[q] >> kSliceLog2) - (FULL ? 0u : a.b0);
-                const uint32_t off = pos[q] & kSliceMask;
-                if (got[q] < R4) {
-                    *(uint32_t*)((char*)sm + (b * R4 + got[q])) = off;
-                } else {
-                    or_pos_global(a.gw, a.b0 + b, off);
+            if (EXACT || (uint32_t)q < k) {
+                const uint32_t b = pos[q] >> kSliceLog2;
+                uint32_t x = got[q] & 0xFFFFu;
+                x = min(x, x - R4);
+                const uint32_t tgt = got[q] < lim ? b * R4 + x : nb * R4;
+                if (LSMB_ABL & 2)
+                    gmax ^= tgt;
+                else
+                    *(uint32_t*)((char*)sm + tgt) = pos[q] & kSliceMask;
+                if (!(LSMB_ABL & 2)) gmax = max(gmax, got[q]);
+            }
+        }
+        if (__builtin_expect(__ballot(gmax >= lim) != 0, 0)) {
+#pragma unroll
+            for (int q = 0; q < KMAX; q++)
+                if ((EXACT || (uint32_t)q < k) && got[q] >= lim && pos[q] < sink) {
+                    or_pos_global(a.gw, a.b0 + (pos[q] >> kSliceLog2), pos[q] & kSliceMask);
 #ifdef LSMB_STATS
                     atomicAdd(a.err + 9, 1u);
 #endif
                 }
-            }
         }
-#pragma unroll
-        for (int q = 0; q < KMAX; q++) pos[q] = npos[q];
-        __syncthreads();
+        walk_positions(nh, nok, pos);
+        kinc = nok ? kInc : 0u;
+        lds_barrier();
 
-        // Flush the owned slices' full segments.
-        uint32_t cnt = 0, nf = 0, sg0 = 0;
+        // Flush: up to 32 full segments per wave per phase (two lanes each);
+        // segments past that stay in their rings for the next phase.
+        uint32_t cnt = 0, nf = 0;
         if (owner) {
-            cnt = min(fill[own], R4) >> 2;
+            cnt = min(fill[own] >> 16, R);
             nf = cnt / (uint32_t)kSegEntries;
-            sg0 = segs[own];
-        }
-        for (uint32_t j = 0; __ballot(j < nf); j++) {
-            const bool has = j < nf;
-            const uint64_t bal = __ballot(has);
-            const uint32_t total = (uint32_t)__popcll(bal);
-            if (has) {
-                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                jobs[rank] = own | (j << 11) | ((sg0 + j) << 16);
+            if (LSMB_ABL & 1) {
+                fill[own] = start;
+                cnt = nf = 0;
             }
-            for (uint32_t r = 0; r < total; r += 16) {
-                const uint32_t jj = r + (lane >> 2), piece = lane & 3;
-                if (jj < total) {
-                    const uint32_t J = jobs[jj];
-                    const uint32_t b = J & 2047u, rj = (J >> 11) & 31u, sg = J >> 16;
-                    const uint32_t* e = sm + b * R + rj * kSegEntries + 2 * piece;
-                    const uint2 x = *(const uint2*)e, y = *(const uint2*)(e + 8), z = *(const uint2*)(e + 16);
-                    const uint64_t w0 = (uint64_t)x.x | ((uint64_t)y.x << 20) | ((uint64_t)z.x << 40);
-                    const uint64_t w1 = (uint64_t)x.y | ((uint64_t)y.y << 20) | ((uint64_t)z.y << 40);
-                    if (sg < a.cap) {
-                        uint4* dst = reinterpret_cast<uint4*>(region_ptr(a, a.b0 + b, w) + (uint64_t)sg * kSegWords) + piece;
-                        *dst = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
-                    } else {  // region full (adversarial inputs): exact global atomics
-                        const uint32_t vals[6] = {x.x, y.x, z.x, x.y, y.y, z.y};
+        }
+        uint32_t excl = 0, total = 0;  // wave prefix sum / sum of nf, bit by bit
+        {
+            const uint32_t lt_lo = __builtin_amdgcn_mbcnt_lo(~0u, 0u);
 #pragma unroll
-                        for (int t = 0; t < 6; t++) or_pos_global(a.gw, a.b0 + b, vals[t]);
+            for (int bit = 0; bit < 6; bit++) {
+                const uint64_t bb = __ballot((nf >> bit) & 1);
+                const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bb >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)bb, 0u));
+                excl += below << bit;
+                total += (uint32_t)__popcll(bb) << bit;
+            }
+            (void)lt_lo;
+        }
+        const uint32_t take = excl >= 32 ? 0u : min(nf, 32u - excl);
+        const uint32_t r8 = R / 8;
+        for (uint32_t j = 0; j < take; j++) {
+            uint32_t u = start / 32 + 3 * j;  // < 2 * r8: one conditional subtract
+            u = min(u, u - r8);
+            jobs[excl + j] = own | (u << 10) | ((segs + j) << 17);
+        }
+        {
+            const uint32_t jj = lane >> 1, hf = lane & 1;
+            const bool act = jj < min(total, 32u);
+            const uint32_t J = jobs[jj];
+            const uint32_t b = act ? J & 1023u : 0u, sg = J >> 17;
+            uint32_t u0 = act ? (J >> 10) & 127u : 0u, u1 = u0 + 1, u2 = u0 + 2;
+            u1 = min(u1, u1 - r8);
+            u2 = min(u2, u2 - r8);
+            const char* base = (const char*)sm + b * R4 + 16 * hf;
+            const uint4 x = *(const uint4*)(base + 32 * u0);
+            const uint4 y = *(const uint4*)(base + 32 * u1);
+            const uint4 z = *(const uint4*)(base + 32 * u2);
+            const uint64_t q0 = pack3(x.x, y.x, z.x), q1 = pack3(x.y, y.y, z.y);
+            const uint64_t q2 = pack3(x.z, y.z, z.z), q3 = pack3(x.w, y.w, z.w);
+            const bool full = act && sg >= a.cap;
+            uint4* dst = act && !full ? reinterpret_cast<uint4*>(region_ptr(a, a.b0 + b, w) + (uint64_t)sg * kSegWords + 4 * hf)
+                                      : dummy;
+            if (!(LSMB_ABL & 8)) {
+                dst[0] = make_uint4((uint32_t)q0, (uint32_t)(q0 >> 32), (uint32_t)q1, (uint32_t)(q1 >> 32));
+                dst[1] = make_uint4((uint32_t)q2, (uint32_t)(q2 >> 32), (uint32_t)q3, (uint32_t)(q3 >> 32));
+            } else if (q0 == 0x123456789ull) {
+                dst[0] = make_uint4(0, 0, 0, 0);
+            }
+            if (__builtin_expect(__ballot(full) != 0, 0)) {
+                if (full) {  // region full (adversarial inputs): exact global atomics
+                    const uint32_t vals[12] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w, z.x, z.y, z.z, z.w};
+#pragma unroll
+                    for (int t = 0; t < 12; t++) or_pos_global(a.gw, a.b0 + b, vals[t]);
 #ifdef LSMB_STATS
-                        atomicAdd(a.err + 7, 6u);
+                    atomicAdd(a.err + 7, 12u);
 #endif
-                    }
                 }
             }
         }
-        if (owner && nf) {
-            // Remainder to the front of the ring (source starts at entry >= 24,
-            // so it never overlaps the destination; reading up to 3 entries
-            // past the fill is harmless).
-            const uint32_t rem = cnt - nf * (uint32_t)kSegEntries;
-            const uint4* s4 = reinterpret_cast<const uint4*>(sm + own * R + nf * kSegEntries);
-            uint4* d4 = reinterpret_cast<uint4*>(sm + own * R);
-            for (uint32_t c = 0; c < rem; c += 4) d4[c >> 2] = s4[c >> 2];
-            fill[own] = rem * 4;
-            segs[own] = min(sg0 + nf, a.cap);  // keeps job words' 16-bit segment field exact
+        if (owner && take) {
+            uint32_t s = start + 96 * take;  // 96*take <= R4: one conditional subtract
+            start = min(s, s - R4);
+            const uint32_t rem = cnt - take * (uint32_t)kSegEntries;
+            fill[own] = (start + 4 * rem) | (rem << 16);
+            segs = min(segs + take, a.cap);  // keeps the job word's segment field exact
         }
-        __syncthreads();
+        lds_barrier();
+    };
+    // Whole groups of kAhead phases (the last group's extra phases carry no
+    // keys): no early exit, so the buffers keep their registers.
+    const uint64_t groups = (iters + kAhead - 1) / kAhead;
+    for (uint64_t g = 0; g < groups; g++) {
+        const uint64_t it = g * kAhead;
+        phase(it, pb1);
+        phase(it + 1, pb2);
+        phase(it + 2, pb3);
+        phase(it + 3, pb0);
     }
 
-    // The last open segment of each owned slice (fill < 24 entries), padded
-    // with copies of its first offset (setting a bit twice is a no-op), and
-    // the region's segment count.
+    // Segments still queued, then the last open segment (< 24 entries, padded
+    // with copies of its first offset: setting a bit twice is a no-op), then
+    // the region's segment count.  Rare tail work, one lane per slice.
     if (owner) {
-        const uint32_t cnt = fill[own] >> 2;
-        uint32_t sg = segs[own];
-        if (cnt) {
-            const uint32_t* e = sm + own * R;
+        uint32_t cnt = min(fill[own] >> 16, R);
+        while (cnt) {
+            const uint32_t m = min(cnt, (uint32_t)kSegEntries);
             uint32_t v[kSegEntries];
 #pragma unroll
-            for (int t = 0; t < kSegEntries; t++) v[t] = (uint32_t)t < cnt ? e[t] : e[0];
-            if (sg < a.cap) {
-                uint64_t* dst = region_ptr(a, a.b0 + own, w) + (uint64_t)sg * kSegWords;
-#pragma unroll
-                for (int t = 0; t < kSegWords; t++)
-                    dst[t] = (uint64_t)v[t] | ((uint64_t)v[t + 8] << 20) | ((uint64_t)v[t + 16] << 40);
-            } else {
-                for (uint32_t t = 0; t < cnt; t++) or_pos_global(a.gw, a.b0 + own, v[t]);
+            for (int t = 0; t < kSegEntries; t++) {
+                uint32_t s = start + 4 * ((uint32_t)t < m ? t : 0);
+                s = min(s, s - R4);
+                v[t] = *(const uint32_t*)((const char*)sm + own * R4 + s);
             }
-            sg++;
+            if (segs < a.cap) {
+                uint64_t* dst = region_ptr(a, a.b0 + own, w) + (uint64_t)segs * kSegWords;
+#pragma unroll
+                for (int t = 0; t < kSegWords; t++) dst[t] = pack3(v[t], v[t + 8], v[t + 16]);
+                segs++;
+            } else {
+                for (uint32_t t = 0; t < m; t++) or_pos_global(a.gw, a.b0 + own, v[t]);
+            }
+            const uint32_t s = start + 4 * m;
+            start = min(s, s - R4);
+            cnt -= m;
         }
-        a.counts[(uint64_t)(a.b0 + own) * a.grid + w] = min(sg, a.cap);
+        a.counts[(uint64_t)(a.b0 + own) * a.grid + w] = segs;
     }
 }
 
@@ -399,22 +488,25 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
             a.counts = ws.counts;
             a.gw = gw;
             a.err = ws.err;
-            const size_t smem = (size_t)a.nb * (4 * a.ring + kBinExtraBytes) + (kBinBlock / 64) * kJobSlots * 4;
+            a.dummy = reinterpret_cast<uint64_t*>(ws.counts + (((size_t)pl.nbins * pl.grid + 63) & ~(size_t)63));
+            const size_t smem = (size_t)(a.nb + 1) * (4 * a.ring + kBinExtraBytes) + (kBinBlock / 64) * kJobSlots * 4;
             auto go = [&](auto kern) {
                 hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
                 kern<<<dim3(pl.grid), dim3(kBinBlock), smem, st>>>(src, n, md, k, a);
             };
             const bool full = pl.sweeps == 1;
-            if (k <= 8) {
+            if (k == 7) {
                 if (w32) {
-                    if (full) go(k_bin<Src, Walk32, 8, true>); else go(k_bin<Src, Walk32, 8, false>);
+                    if (full) go(k_bin<Src, Walk32, 7, true, true>); else go(k_bin<Src, Walk32, 7, true, false>);
                 } else {
-                    if (full) go(k_bin<Src, Walk64, 8, true>); else go(k_bin<Src, Walk64, 8, false>);
+                    if (full) go(k_bin<Src, Walk64, 7, true, true>); else go(k_bin<Src, Walk64, 7, true, false>);
                 }
+            } else if (k <= 8) {
+                if (w32) go(k_bin<Src, Walk32, 8, false, false>); else go(k_bin<Src, Walk64, 8, false, false>);
             } else if (k <= 16) {
-                if (w32) go(k_bin<Src, Walk32, 16, false>); else go(k_bin<Src, Walk64, 16, false>);
+                if (w32) go(k_bin<Src, Walk32, 16, false, false>); else go(k_bin<Src, Walk64, 16, false, false>);
             } else {
-                if (w32) go(k_bin<Src, Walk32, 32, false>); else go(k_bin<Src, Walk64, 32, false>);
+                if (w32) go(k_bin<Src, Walk32, 32, false, false>); else go(k_bin<Src, Walk64, 32, false, false>);
             }
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
@@ -463,16 +555,16 @@ PartitionPlan plan_partition(uint32_t num_bits, uint32_t k, uint64_t n, int num_
     // with margin.  Claims past the ring fall back to exact global atomics.
     const double lambda = (double)kBinBlock * k * fmin(1.0, (double)(1u << kSliceLog2) / (double)num_bits);
     uint32_t need = kSegEntries + (uint32_t)ceil(lambda + 2.0 * sqrt(lambda));
-    need = (need + 3) & ~3u;
-    if (need > kMaxRing) need = kMaxRing & ~3u;
+    need = (need + 7) & ~7u;
+    if (need > kMaxRing) need = kMaxRing;
     // Fewest sweeps whose slices fit LDS with that ring; each sweep re-reads
     // and re-hashes the keys and keeps only its own slices' positions.
     pl.sweeps = (pl.nbins + kMaxBinsPerSweep - 1) / kMaxBinsPerSweep;
     for (;; pl.sweeps++) {
         pl.bins_per_sweep = (pl.nbins + pl.sweeps - 1) / pl.sweeps;
-        uint32_t r = (kBinLdsBudget / pl.bins_per_sweep - kBinExtraBytes) / 4;
-        r &= ~3u;
-        if (r > kMaxRing) r = kMaxRing & ~3u;
+        uint32_t r = (kBinLdsBudget / (pl.bins_per_sweep + 1) - kBinExtraBytes) / 4;  // + the sink slice
+        r &= ~7u;
+        if (r > kMaxRing) r = kMaxRing;
         if (r >= need || pl.bins_per_sweep == 1) {
             pl.ring = r;
             break;
@@ -493,7 +585,8 @@ PartitionPlan plan_partition(uint32_t num_bits, uint32_t k, uint64_t n, int num_
     // A region holds at most kMaxRegionSegs segments (pass A's job word);
     // a bigger plan is reported as unbounded so callers chunk the keys.
     pl.region_bytes = pl.cap_segs > kMaxRegionSegs ? ~0ull >> 2 : (uint64_t)pl.nbins * pl.grid * pl.cap_segs * 64;
-    pl.counts_bytes = (uint64_t)pl.nbins * pl.grid * 4;
+    // + pass A's dummy store slots (32 B per thread), 256-B aligned
+    pl.counts_bytes = (((uint64_t)pl.nbins * pl.grid + 63) & ~63ull) * 4 + (uint64_t)pl.grid * kBinBlock * 32;
     return pl;
 }
 

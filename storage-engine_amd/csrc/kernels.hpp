@@ -20,10 +20,10 @@ constexpr uint32_t kLdsFilterMaxWords32 = 40 * 1024;  // 160 KiB: whole filter i
 constexpr uint32_t kLdsBytes = 160 * 1024;            // LDS per CU (gfx950)
 constexpr uint32_t kJobSlots = 64;                    // pass A: per-wave flush job list (u32 each)
 constexpr uint32_t kBinLdsBudget = kLdsBytes - (kBinBlock / 64) * kJobSlots * 4;  // rings + per-slice words
-constexpr uint32_t kBinExtraBytes = 8;                // per slice besides its ring: fill + segments written
+constexpr uint32_t kBinExtraBytes = 4;                // per slice besides its ring: fill word
 constexpr uint32_t kMaxBinsPerSweep = 1024;           // one owner lane per slice: <= 64 slices per wave
-constexpr uint32_t kMaxRing = 31 * kSegEntries;       // ring entries per slice (job word: 5-bit ring segment)
-constexpr uint32_t kMaxRegionSegs = 65000;            // job word: 16-bit region segment index (+ ring segments)
+constexpr uint32_t kMaxRing = 8 * 127;                // ring entries per slice (job word: 7-bit 32-B ring unit)
+constexpr uint32_t kMaxRegionSegs = 32000;            // job word: 15-bit region segment index (+ ring segments)
 
 // How a key batch is presented to the kernels.
 struct KeyBatch {
