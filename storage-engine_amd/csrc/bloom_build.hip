@@ -31,7 +31,8 @@
 #include "keysrc.hpp"
 
 // LSMB_ABL (timing ablations for tools/, never in the product build):
-//   1 = no segment flush, 2 = no claims/stores, 8 = no region stores.
+//   1 = no segment flush, 2 = no claims/stores, 8 = no region stores,
+//   16 = region stores issued but all dropped (out-of-range offset).
 #ifndef LSMB_ABL
 #define LSMB_ABL 0
 #endif
@@ -89,17 +90,17 @@ __global__ __launch_bounds__(256) void k_build_atomic(Src src, uint64_t n, Mod32
 // ---------------------------------------------------------------- Partition strategy
 struct PassA {
     uint32_t b0, nb;        // this sweep's slices [b0, b0 + nb)
+    uint32_t nbins;         // slices of the whole filter
     uint32_t grid, cap;     // regions per slice, region capacity (segments)
     uint32_t ring;          // ring entries per slice (multiple of 8, >= kSegEntries)
-    uint64_t* regions;      // [nbins][grid][cap][8] u64
+    uint64_t* regions;      // [grid][nbins][cap][8] u64: workgroup w's regions are contiguous
     uint32_t* counts;       // [nbins][grid] segments written
     uint32_t* gw;           // filter words (ring / region overflow only)
     uint32_t* err;          // device counters (LSMB_STATS builds)
-    uint64_t* dummy;        // [grid][kBinBlock][4] u64: stores of lanes without a flush job
 };
 
 __device__ __forceinline__ uint64_t* region_ptr(const PassA& a, uint32_t b, uint32_t w) {
-    return a.regions + ((uint64_t)b * a.grid + w) * a.cap * kSegWords;
+    return a.regions + ((uint64_t)w * a.nbins + b) * a.cap * kSegWords;
 }
 
 // Workgroup barrier that waits for this wave's LDS operations only.
@@ -156,16 +157,16 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
     const uint32_t R = a.ring, R4 = 4 * a.ring, nb = a.nb;
     uint32_t* fill = sm + (size_t)(nb + 1) * R;  // nb + 1 fill words (the last: sink)
     const uint32_t tid = threadIdx.x, w = blockIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint32_t* jobs = fill + nb + 1 + wave * kJobSlots;
     for (uint32_t i = tid; i <= nb; i += kBinBlock) fill[i] = 0;
-    for (uint32_t i = tid; i < (kBinBlock / 64) * kJobSlots; i += kBinBlock) fill[nb + 1 + i] = 0;
+    // Workgroup w's regions as a raw buffer: a store at an offset past
+    // num_records is dropped by the hardware, which lets every lane issue the
+    // flush stores unconditionally (see the flush).
+    const __amdgpu_buffer_rsrc_t rgn = __builtin_amdgcn_make_buffer_rsrc(
+        region_ptr(a, 0, w), 0, (int)(a.nbins * a.cap * 64u), 0x00020000);
+    constexpr uint32_t kDrop = 0x80000000u;  // >= num_records (plan keeps it < 2^31)
     constexpr uint32_t kInc = 4u | (1u << 16);
     const uint32_t sink = nb << kSliceLog2;  // local position of the sink slice
     const uint32_t lim = R << 16;            // fill < lim <=> claims < R
-    // Where lanes without a flush job store (keeps the store count static):
-    // 32 B per thread, so the stores never contend for one address and stay
-    // in L2 (plain stores, rewritten every phase).
-    uint4* const dummy = reinterpret_cast<uint4*>(a.dummy) + ((uint64_t)w * kBinBlock + tid) * 2;
 
     // Workgroup w owns keys [w*per, (w+1)*per): a contiguous, coalesced run.
     const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
@@ -257,77 +258,77 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
         kinc = nok ? kInc : 0u;
         lds_barrier();
 
-        // Flush: up to 32 full segments per wave per phase (two lanes each);
-        // segments past that stay in their rings for the next phase.
-        uint32_t cnt = 0, nf = 0;
+        // Flush: each owner lane writes its slice's full segment (usually
+        // none or one) to the region, 4 x 16 B.  The four stores are issued
+        // by every lane, at a dropped offset where there is nothing to write:
+        // with a static store count per phase the compiler's vmcnt waits for
+        // the prefetched keys stay counted (a conditional store would make
+        // them drain the latest phase's stores).
+        uint32_t cnt = 0;
         if (owner) {
             cnt = min(fill[own] >> 16, R);
-            nf = cnt / (uint32_t)kSegEntries;
             if (LSMB_ABL & 1) {
                 fill[own] = start;
-                cnt = nf = 0;
+                cnt = 0;
             }
         }
-        uint32_t excl = 0, total = 0;  // wave prefix sum / sum of nf, bit by bit
-        {
-            const uint32_t lt_lo = __builtin_amdgcn_mbcnt_lo(~0u, 0u);
-#pragma unroll
-            for (int bit = 0; bit < 6; bit++) {
-                const uint64_t bb = __ballot((nf >> bit) & 1);
-                const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bb >> 32),
-                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)bb, 0u));
-                excl += below << bit;
-                total += (uint32_t)__popcll(bb) << bit;
-            }
-            (void)lt_lo;
-        }
-        const uint32_t take = excl >= 32 ? 0u : min(nf, 32u - excl);
-        const uint32_t r8 = R / 8;
-        for (uint32_t j = 0; j < take; j++) {
-            uint32_t u = start / 32 + 3 * j;  // < 2 * r8: one conditional subtract
-            u = min(u, u - r8);
-            jobs[excl + j] = own | (u << 10) | ((segs + j) << 17);
-        }
-        {
-            const uint32_t jj = lane >> 1, hf = lane & 1;
-            const bool act = jj < min(total, 32u);
-            const uint32_t J = jobs[jj];
-            const uint32_t b = act ? J & 1023u : 0u, sg = J >> 17;
-            uint32_t u0 = act ? (J >> 10) & 127u : 0u, u1 = u0 + 1, u2 = u0 + 2;
-            u1 = min(u1, u1 - r8);
-            u2 = min(u2, u2 - r8);
-            const char* base = (const char*)sm + b * R4 + 16 * hf;
-            const uint4 x = *(const uint4*)(base + 32 * u0);
-            const uint4 y = *(const uint4*)(base + 32 * u1);
-            const uint4 z = *(const uint4*)(base + 32 * u2);
-            const uint64_t q0 = pack3(x.x, y.x, z.x), q1 = pack3(x.y, y.y, z.y);
-            const uint64_t q2 = pack3(x.z, y.z, z.z), q3 = pack3(x.w, y.w, z.w);
-            const bool full = act && sg >= a.cap;
-            uint4* dst = act && !full ? reinterpret_cast<uint4*>(region_ptr(a, a.b0 + b, w) + (uint64_t)sg * kSegWords + 4 * hf)
-                                      : dummy;
+        const bool has = cnt >= (uint32_t)kSegEntries;
+        const char* ring = (const char*)sm + own * R4;
+        uint4 x0, x1, y0, y1, z0, z1;
+        auto read_segment = [&]() {
+            // the segment's three 8-entry groups (8 | R: a group never wraps)
+            uint32_t g0 = start, g1 = start + 32, g2 = start + 64;
+            g1 = min(g1, g1 - R4);
+            g2 = min(g2, g2 - R4);
+            x0 = *(const uint4*)(ring + g0), x1 = *(const uint4*)(ring + g0 + 16);
+            y0 = *(const uint4*)(ring + g1), y1 = *(const uint4*)(ring + g1 + 16);
+            z0 = *(const uint4*)(ring + g2), z1 = *(const uint4*)(ring + g2 + 16);
+        };
+        auto store_segment = [&](uint32_t off) {
+            const uint64_t q0 = pack3(x0.x, y0.x, z0.x), q1 = pack3(x0.y, y0.y, z0.y);
+            const uint64_t q2 = pack3(x0.z, y0.z, z0.z), q3 = pack3(x0.w, y0.w, z0.w);
+            const uint64_t q4 = pack3(x1.x, y1.x, z1.x), q5 = pack3(x1.y, y1.y, z1.y);
+            const uint64_t q6 = pack3(x1.z, y1.z, z1.z), q7 = pack3(x1.w, y1.w, z1.w);
             if (!(LSMB_ABL & 8)) {
-                dst[0] = make_uint4((uint32_t)q0, (uint32_t)(q0 >> 32), (uint32_t)q1, (uint32_t)(q1 >> 32));
-                dst[1] = make_uint4((uint32_t)q2, (uint32_t)(q2 >> 32), (uint32_t)q3, (uint32_t)(q3 >> 32));
-            } else if (q0 == 0x123456789ull) {
-                dst[0] = make_uint4(0, 0, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{(uint32_t)q0, (uint32_t)(q0 >> 32), (uint32_t)q1, (uint32_t)(q1 >> 32)}, rgn, off, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{(uint32_t)q2, (uint32_t)(q2 >> 32), (uint32_t)q3, (uint32_t)(q3 >> 32)}, rgn, off + 16, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{(uint32_t)q4, (uint32_t)(q4 >> 32), (uint32_t)q5, (uint32_t)(q5 >> 32)}, rgn, off + 32, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{(uint32_t)q6, (uint32_t)(q6 >> 32), (uint32_t)q7, (uint32_t)(q7 >> 32)}, rgn, off + 48, 0, 0);
             }
-            if (__builtin_expect(__ballot(full) != 0, 0)) {
-                if (full) {  // region full (adversarial inputs): exact global atomics
-                    const uint32_t vals[12] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w, z.x, z.y, z.z, z.w};
-#pragma unroll
-                    for (int t = 0; t < 12; t++) or_pos_global(a.gw, a.b0 + b, vals[t]);
+        };
+        auto spill_segment = [&]() {  // region full (adversarial inputs): exact global atomics
+            const uint32_t vals[24] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w,
+                                       y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w,
+                                       z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
+            for (int t = 0; t < 24; t++) or_pos_global(a.gw, a.b0 + own, vals[t]);
 #ifdef LSMB_STATS
-                    atomicAdd(a.err + 7, 12u);
+            atomicAdd(a.err + 7, 24u);
 #endif
-                }
-            }
+        };
+        if (has) read_segment();
+        {
+            const bool real = !(LSMB_ABL & 16) && has && segs < a.cap;
+            store_segment(real ? ((a.b0 + own) * a.cap + segs) * 64u : kDrop);
         }
-        if (owner && take) {
-            uint32_t s = start + 96 * take;  // 96*take <= R4: one conditional subtract
+        if (has) {
+            if (segs >= a.cap) spill_segment();
+            const uint32_t nf = cnt / (uint32_t)kSegEntries;
+            uint32_t s = start + 96;
             start = min(s, s - R4);
-            const uint32_t rem = cnt - take * (uint32_t)kSegEntries;
+            segs = min(segs + 1, a.cap);
+            // more full segments (filters with few, busy slices)
+            for (uint32_t j = 1; j < nf; j++) {
+                read_segment();
+                if (segs < a.cap)
+                    store_segment(((a.b0 + own) * a.cap + segs) * 64u);
+                else
+                    spill_segment();
+                s = start + 96;
+                start = min(s, s - R4);
+                segs = min(segs + 1, a.cap);
+            }
+            const uint32_t rem = cnt - nf * (uint32_t)kSegEntries;
             fill[own] = (start + 4 * rem) | (rem << 16);
-            segs = min(segs + take, a.cap);  // keeps the job word's segment field exact
         }
         lds_barrier();
     };
@@ -389,7 +390,7 @@ __global__ __launch_bounds__(kApplyBlock) void k_apply(const uint64_t* __restric
         __syncthreads();
         for (uint32_t r = wave; r < grid; r += NWAVE) {
             const uint32_t nseg = counts[(uint64_t)b * grid + r];
-            const uint4* src = reinterpret_cast<const uint4*>(regions + ((uint64_t)b * grid + r) * cap * kSegWords);
+            const uint4* src = reinterpret_cast<const uint4*>(regions + ((uint64_t)r * nbins + b) * cap * kSegWords);
             const uint32_t n16 = nseg * (kSegWords / 2);  // 16-B pieces (2 words, 6 offsets)
             constexpr uint32_t U = 4;                      // loads in flight per lane
             for (uint32_t i0 = 0; i0 < n16; i0 += 64 * U) {
@@ -488,8 +489,8 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
             a.counts = ws.counts;
             a.gw = gw;
             a.err = ws.err;
-            a.dummy = reinterpret_cast<uint64_t*>(ws.counts + (((size_t)pl.nbins * pl.grid + 63) & ~(size_t)63));
-            const size_t smem = (size_t)(a.nb + 1) * (4 * a.ring + kBinExtraBytes) + (kBinBlock / 64) * kJobSlots * 4;
+            a.nbins = pl.nbins;
+            const size_t smem = (size_t)(a.nb + 1) * (4 * a.ring + kBinExtraBytes);
             auto go = [&](auto kern) {
                 hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
                 kern<<<dim3(pl.grid), dim3(kBinBlock), smem, st>>>(src, n, md, k, a);
@@ -582,11 +583,12 @@ PartitionPlan plan_partition(uint32_t num_bits, uint32_t k, uint64_t n, int num_
     const double mu = (double)keys_w * k * p;
     const double cap_e = mu + 8.0 * sqrt(mu) + 2.0 * kSegEntries;
     pl.cap_segs = (uint32_t)ceil(cap_e / kSegEntries);
-    // A region holds at most kMaxRegionSegs segments (pass A's job word);
+    // A region holds at most kMaxRegionSegs segments
     // a bigger plan is reported as unbounded so callers chunk the keys.
-    pl.region_bytes = pl.cap_segs > kMaxRegionSegs ? ~0ull >> 2 : (uint64_t)pl.nbins * pl.grid * pl.cap_segs * 64;
-    // + pass A's dummy store slots (32 B per thread), 256-B aligned
-    pl.counts_bytes = (((uint64_t)pl.nbins * pl.grid + 63) & ~63ull) * 4 + (uint64_t)pl.grid * kBinBlock * 32;
+    // (and a workgroup's regions within pass A's 2^31-byte buffer range)
+    const bool fits = pl.cap_segs <= kMaxRegionSegs && (uint64_t)pl.nbins * pl.cap_segs * 64 < (1ull << 31);
+    pl.region_bytes = fits ? (uint64_t)pl.nbins * pl.grid * pl.cap_segs * 64 : ~0ull >> 2;
+    pl.counts_bytes = (uint64_t)pl.nbins * pl.grid * 4;
     return pl;
 }
 

@@ -18,12 +18,11 @@ constexpr int kBinBlock = 1024;                       // pass A workgroup
 constexpr int kApplyBlock = 1024;                     // pass B workgroup
 constexpr uint32_t kLdsFilterMaxWords32 = 40 * 1024;  // 160 KiB: whole filter in LDS
 constexpr uint32_t kLdsBytes = 160 * 1024;            // LDS per CU (gfx950)
-constexpr uint32_t kJobSlots = 64;                    // pass A: per-wave flush job list (u32 each)
-constexpr uint32_t kBinLdsBudget = kLdsBytes - (kBinBlock / 64) * kJobSlots * 4;  // rings + per-slice words
+constexpr uint32_t kBinLdsBudget = kLdsBytes;         // pass A: rings + fill words
 constexpr uint32_t kBinExtraBytes = 4;                // per slice besides its ring: fill word
 constexpr uint32_t kMaxBinsPerSweep = 1024;           // one owner lane per slice: <= 64 slices per wave
-constexpr uint32_t kMaxRing = 8 * 127;                // ring entries per slice (job word: 7-bit 32-B ring unit)
-constexpr uint32_t kMaxRegionSegs = 32000;            // job word: 15-bit region segment index (+ ring segments)
+constexpr uint32_t kMaxRing = 1024;                   // ring entries per slice
+constexpr uint32_t kMaxRegionSegs = 1u << 24;         // region capacity bound (segments)
 
 // How a key batch is presented to the kernels.
 struct KeyBatch {
