@@ -36,6 +36,9 @@
 #ifndef LSMB_ABL
 #define LSMB_ABL 0
 #endif
+#ifndef LSMB_APPLY_U
+#define LSMB_APPLY_U 8  // pass B: 16-B region loads in flight per lane
+#endif
 
 namespace lsmb {
 namespace {
@@ -392,7 +395,7 @@ __global__ __launch_bounds__(kApplyBlock) void k_apply(const uint64_t* __restric
             const uint32_t nseg = counts[(uint64_t)b * grid + r];
             const uint4* src = reinterpret_cast<const uint4*>(regions + ((uint64_t)r * nbins + b) * cap * kSegWords);
             const uint32_t n16 = nseg * (kSegWords / 2);  // 16-B pieces (2 words, 6 offsets)
-            constexpr uint32_t U = 4;                      // loads in flight per lane
+            constexpr uint32_t U = LSMB_APPLY_U;           // loads in flight per lane
             for (uint32_t i0 = 0; i0 < n16; i0 += 64 * U) {
                 uint4 v[U];
 #pragma unroll
