@@ -208,6 +208,10 @@ const char* lsmb_build_strategy(uint32_t num_bits, uint64_t n);
  * [2] pass B (apply).  Valid after lsmb_sync. */
 int lsmb_last_build_ms(lsmb_ctx* ctx, float* out3);
 
+/* Per-build HIP events behind lsmb_last_build_ms: on (1, the default) or off
+ * (0: a build issues only its kernels, no timing markers between them). */
+int lsmb_set_timing(lsmb_ctx* ctx, int enable);
+
 #ifdef __cplusplus
 }
 #endif

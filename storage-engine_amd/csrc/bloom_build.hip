@@ -27,6 +27,9 @@
 //              atomics on the filter (the memory-side atomic unit serves ~20 G
 //              scattered requests/s chip-wide; 7e8 of them would take ~35 ms).
 //   Atomic     few keys into a huge filter: direct global atomicOr.
+#include <mutex>
+#include <vector>
+
 #include "kernels.hpp"
 #include "keysrc.hpp"
 
@@ -377,6 +380,14 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
 }
 
 // Pass B: one 2^20-bit slice per workgroup, applied in LDS.
+//   1. the slice's words go to LDS with every load issued before the first
+//      LDS write (a load / wait / write loop pays one HBM round trip per 8 B
+//      of each thread: 16 per slice);
+//   2. wave v applies regions v, v+16, ...; their segment counts arrive in
+//      one lane-parallel load up front (lane j: region v + 16 j), then each
+//      region's 16-B pieces are loaded U per lane at a time and every 20-bit
+//      offset is ORed into LDS;
+//   3. the slice is written back once.
 __global__ __launch_bounds__(kApplyBlock) void k_apply(const uint64_t* __restrict__ regions,
                                                        const uint32_t* __restrict__ counts,
                                                        uint32_t grid, uint32_t cap, uint32_t nbins,
@@ -384,15 +395,31 @@ __global__ __launch_bounds__(kApplyBlock) void k_apply(const uint64_t* __restric
     __shared__ uint32_t filt[kSliceWords32];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr uint32_t NWAVE = kApplyBlock / 64;
+    constexpr uint32_t PER = kSliceWords32 / 2 / kApplyBlock;  // u64 words per thread
     for (uint32_t b = blockIdx.x; b < nbins; b += gridDim.x) {
         const uint64_t w0 = (uint64_t)b * kSliceWords32;
-        const uint32_t nw = (uint32_t)min((uint64_t)kSliceWords32, nw32 - w0);  // even
+        const uint32_t nw2 = (uint32_t)min((uint64_t)kSliceWords32, nw32 - w0) / 2;  // u64 words
         uint2* g2 = reinterpret_cast<uint2*>(gw + w0);
         uint2* f2 = reinterpret_cast<uint2*>(filt);
-        for (uint32_t i = tid; i < nw / 2; i += kApplyBlock) f2[i] = g2[i];
+        {
+            uint2 v[PER];
+#pragma unroll
+            for (uint32_t u = 0; u < PER; u++) {
+                const uint32_t i = tid + u * kApplyBlock;
+                v[u] = i < nw2 ? g2[i] : make_uint2(0, 0);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < PER; u++) {
+                const uint32_t i = tid + u * kApplyBlock;
+                if (i < nw2) f2[i] = v[u];
+            }
+        }
+        const uint32_t nreg = wave < grid ? (grid - 1 - wave) / NWAVE + 1 : 0;  // <= 64 (grid <= 1024)
+        const uint32_t cnt = lane < nreg ? counts[(uint64_t)b * grid + wave + lane * NWAVE] : 0u;
         __syncthreads();
-        for (uint32_t r = wave; r < grid; r += NWAVE) {
-            const uint32_t nseg = counts[(uint64_t)b * grid + r];
+        for (uint32_t j = 0; j < nreg; j++) {
+            const uint32_t r = wave + j * NWAVE;
+            const uint32_t nseg = __shfl(cnt, (int)j);
             const uint4* src = reinterpret_cast<const uint4*>(regions + ((uint64_t)r * nbins + b) * cap * kSegWords);
             const uint32_t n16 = nseg * (kSegWords / 2);  // 16-B pieces (2 words, 6 offsets)
             constexpr uint32_t U = LSMB_APPLY_U;           // loads in flight per lane
@@ -420,7 +447,7 @@ __global__ __launch_bounds__(kApplyBlock) void k_apply(const uint64_t* __restric
             }
         }
         __syncthreads();
-        for (uint32_t i = tid; i < nw / 2; i += kApplyBlock) g2[i] = f2[i];
+        for (uint32_t i = tid; i < nw2; i += kApplyBlock) g2[i] = f2[i];
         __syncthreads();
     }
 }
@@ -454,6 +481,18 @@ __global__ __launch_bounds__(256) void k_gen_key16(uint64_t seed, uint64_t first
     }
 }
 
+// The max-dynamic-LDS attribute is a property of the kernel, not of a launch:
+// set it once per kernel (to the whole 160 KiB), not before every launch.
+void set_max_lds(const void* fn) {
+    static std::mutex mu;
+    static std::vector<const void*> done;
+    std::lock_guard<std::mutex> g(mu);
+    for (const void* d : done)
+        if (d == fn) return;
+    hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
+    done.push_back(fn);
+}
+
 template <class Src>
 hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k, uint32_t* gw,
                       BuildStrategy s, const PartitionWorkspace& ws, int num_cus, hipStream_t st,
@@ -468,8 +507,7 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
         const uint64_t gmax = (uint64_t)num_cus * (smem <= 40 * 1024 ? 4 : 1);
         if (g > gmax) g = gmax;
         if (g < 1) g = 1;
-        hipFuncSetAttribute((const void*)k_build_lds<Src>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)smem);
+        set_max_lds((const void*)k_build_lds<Src>);
         k_build_lds<Src><<<dim3((uint32_t)g), dim3(1024), smem, st>>>(src, n, md, k, nw32, gw);
         if (tm) hipEventRecord(tm->t1, st);
     } else if (s == BuildStrategy::Atomic) {
@@ -495,7 +533,7 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
             a.nbins = pl.nbins;
             const size_t smem = (size_t)(a.nb + 1) * (4 * a.ring + kBinExtraBytes);
             auto go = [&](auto kern) {
-                hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+                set_max_lds((const void*)kern);
                 kern<<<dim3(pl.grid), dim3(kBinBlock), smem, st>>>(src, n, md, k, a);
             };
             const bool full = pl.sweeps == 1;

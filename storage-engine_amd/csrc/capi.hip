@@ -101,6 +101,7 @@ struct lsmb_ctx {
     ProbeFilter* desc_pinned = nullptr;      // pinned staging for descriptor uploads
     hipEvent_t desc_done = nullptr;          // last kernel that read filt_desc
     std::vector<uint64_t> offs_tmp;
+    bool timing = true;            // per-build HIP events (lsmb_set_timing)
 };
 
 namespace {
@@ -129,8 +130,7 @@ int check_device_error(lsmb_ctx* c) {
     {
         uint32_t st[16];
         HIP_TRY(hipMemcpy(st, c->err.p, 64, hipMemcpyDeviceToHost));
-        fprintf(stderr, "[lsmb stats] deferred=%u region_full=%u stall_passes=%u wave_iters=%u flush_rounds=%u\n",
-                st[9], st[7], st[10], st[11], st[12]);
+        fprintf(stderr, "[lsmb stats] ring_overflow=%u region_full=%u\n", st[9], st[7]);
         HIP_TRY(hipMemset((char*)c->err.p + 4, 0, 60));
     }
 #endif
@@ -148,11 +148,15 @@ int check_device_error(lsmb_ctx* c) {
 // Device build of one batch, chunked so the partition workspace stays bounded.
 int build_dev(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k, uint32_t* dw,
               hipStream_t st) {
-    const BuildStrategy s = pick_build_strategy(num_bits, k, kb_all.n);
+    BuildStrategy s = pick_build_strategy(num_bits, k, kb_all.n);
+    // LSMB_FORCE_STRATEGY=atomic: measurement override;
+    // the filter is the same either way.
+    if (const char* f = getenv("LSMB_FORCE_STRATEGY"))
+        if (s == BuildStrategy::Partition && !strcmp(f, "atomic")) s = BuildStrategy::Atomic;
     c->tm.valid = false;
     if (s == BuildStrategy::None) return LSMB_OK;
     if (s != BuildStrategy::Partition) {
-        HIP_TRY(launch_build(kb_all, num_bits, k, dw, s, PartitionWorkspace{}, c->num_cus, st, &c->tm));
+        HIP_TRY(launch_build(kb_all, num_bits, k, dw, s, PartitionWorkspace{}, c->num_cus, st, c->timing ? &c->tm : nullptr));
         return LSMB_OK;
     }
     uint64_t chunk = partition_chunk_keys(num_bits, k, workspace_limit_bytes(), c->num_cus);
@@ -174,7 +178,7 @@ int build_dev(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k
             kb.offsets += first;  // VarLen offsets are absolute into data
         else
             kb.data += first * kb.key_len;
-        HIP_TRY(launch_build(kb, num_bits, k, dw, s, ws, c->num_cus, st, &c->tm));
+        HIP_TRY(launch_build(kb, num_bits, k, dw, s, ws, c->num_cus, st, c->timing ? &c->tm : nullptr));
     }
     return LSMB_OK;
 }
@@ -576,6 +580,12 @@ int lsmb_gen_key16_dev(lsmb_ctx* c, uint64_t seed, uint64_t first, uint64_t n, v
 
 const char* lsmb_build_strategy(uint32_t num_bits, uint64_t n) {
     return strategy_name(pick_build_strategy(num_bits, 7, n));
+}
+
+int lsmb_set_timing(lsmb_ctx* c, int enable) {
+    if (!c) return fail(LSMB_EINVAL, "null ctx");
+    c->timing = enable != 0;
+    return LSMB_OK;
 }
 
 int lsmb_last_build_ms(lsmb_ctx* c, float* out3) {

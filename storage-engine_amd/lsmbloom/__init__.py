@@ -73,6 +73,7 @@ SIGNATURES = {
     "lsmb_fset_probe_dev": (ctypes.c_int, [vp, vp, vp, ctypes.c_uint32, ctypes.c_uint64, vp, vp]),
     "lsmb_build_strategy": (ctypes.c_char_p, [ctypes.c_uint32, ctypes.c_uint64]),
     "lsmb_last_build_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_float)]),
+    "lsmb_set_timing": (ctypes.c_int, [vp, ctypes.c_int]),
 }
 
 _lib = None
@@ -251,6 +252,10 @@ class Context:
 
     def gen_key16_dev(self, seed, first, n, out, stream=None):
         _check(lib().lsmb_gen_key16_dev(self.h, seed, first, n, vp(out.data_ptr()), self._stream(stream)))
+
+    def set_timing(self, on):
+        """Per-build HIP events (lsmb_last_build_ms) on/off."""
+        _check(lib().lsmb_set_timing(self.h, 1 if on else 0))
 
     def last_build_ms(self):
         a = (ctypes.c_float * 3)()
