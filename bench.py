@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time box")
     ap.add_argument("--verify", action="store_true", help="check the built filter against the oracle")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory end-to-end measurement")
+    ap.add_argument("--no-varlen", action="store_true", help="skip the C4 variable-length build leg")
+    ap.add_argument("--varlen-keys", type=int, default=100_000_000)
     return ap.parse_args()
 
 
@@ -176,6 +178,14 @@ def main():
         out["e2e"] = bench_e2e(ctx, keys, npg, nb, k)
 
     del keys
+    words = None
+    torch.cuda.empty_cache()
+    if not args.no_varlen and world == 1:
+        out["varlen"] = bench_varlen(ctx, dev, args)
+    tr = committed_traffic()
+    if tr:
+        out["roofline"]["traffic"] = tr["bytes"]
+        out["roofline"]["traffic_source"] = tr["source"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(nb, k, args.cpu_seconds)
         out["cpu_baseline"]["gpu_over_cpu_1thread"] = round(value / out["cpu_baseline"]["value"], 1)
@@ -187,31 +197,101 @@ def main():
 
 
 def bench_e2e(ctx, keys, n, nb, k, reps=3):
-    """Keys in host memory -> filter serialized in host memory: the flush path
-    (SSTableBuilder::finish, src/sstable/builder.rs:177-182).  lsmb_build_fixed
-    does H2D of the keys (chunks of 256 MiB), the build kernels and D2H of the
-    words; lsmb_serialize writes the on-disk bloom block (src/bloom/mod.rs:102-115)."""
+    """Keys in host memory -> serialized bloom block in host memory: the flush
+    path (SSTableBuilder::finish, src/sstable/builder.rs:177-182).  One
+    lsmb_build_block call: chunked H2D of the keys overlapped with the build
+    kernels, then D2H of the words straight into the block (no serialize copy).
+    Measured with pageable key memory (a memtable arena) and pinned key memory."""
     import numpy as np
+    import torch
 
     import lsmbloom
-    host = keys.cpu().numpy().reshape(-1)  # pageable host memory, like a memtable arena
-    words = np.zeros(lsmbloom.num_words(nb), dtype=np.uint64)
-    ctx.build_fixed(host, 16, nb, k, words)  # warm-up (allocations)
-    tb, ts = [], []
-    for _ in range(reps):
-        words[:] = 0
-        t0 = time.perf_counter()
-        ctx.build_fixed(host, 16, nb, k, words)
-        t1 = time.perf_counter()
-        blob = lsmbloom.BloomFilter(words, k, nb).serialize()
-        t2 = time.perf_counter()
-        tb.append(t1 - t0)
-        ts.append(t2 - t1)
-    b, s_ = float(np.median(tb)), float(np.median(ts))
-    return {"what": "host keys -> H2D -> build -> D2H words -> serialize (pageable host memory)",
-            "build_ms": round(b * 1e3, 2), "serialize_ms": round(s_ * 1e3, 2),
-            "value": round(n / (b + s_) / 1e6, 1), "unit": "Mkeys/s",
-            "h2d_bytes": n * 16, "d2h_bytes": 8 * lsmbloom.num_words(nb), "serialized_bytes": len(blob)}
+    size = lsmbloom.serialized_size(nb)
+    res = {"what": "host keys -> H2D (chunked, overlapped) -> build -> D2H into the serialized block "
+                   "(lsmb_build_block)", "h2d_bytes": n * 16, "d2h_bytes": size - 12, "serialized_bytes": size}
+    host = keys.cpu().numpy().reshape(-1)
+    for name, src in (("pageable", host), ("pinned", None)):
+        if src is None:
+            pin = torch.empty(host.size, dtype=torch.uint8).pin_memory()
+            pin.numpy()[:] = host
+            src = pin.numpy()
+        block = np.empty(size, dtype=np.uint8)
+        block[:] = 0  # fault the pages in before timing
+        ctx.build_block(src, nb, k, key_len=16, out=block)  # warm-up (staging allocations)
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            ctx.build_block(src, nb, k, key_len=16, out=block)
+            ts.append(time.perf_counter() - t0)
+        t = float(np.median(ts))
+        res[name] = {"ms": round(t * 1e3, 2), "value": round(n / t / 1e6, 1), "unit": "Mkeys/s",
+                     "pcie_GBs": round((n * 16 + size) / t / 1e9, 1)}
+    res["value"] = res["pageable"]["value"]
+    res["unit"] = "Mkeys/s"
+    return res
+
+
+def bench_varlen(ctx, dev, args):
+    """C4 (configs[3]): 100 M variable-length keys (8-256 B, mean 132 B; the
+    tests/keygen.varlen stream), packed data + offsets resident in HBM, into
+    BloomFilter::new(1e8, 0.01)."""
+    import numpy as np
+    import torch
+
+    import lsmbloom
+    n = args.varlen_keys
+    data, offs = ctx.gen_varlen_dev(n, device=dev)
+    nb, k = lsmbloom.params(n, 0.01)
+    nw = lsmbloom.num_words(nb)
+    words = torch.zeros(nw, dtype=torch.int64, device=dev)
+
+    def step():
+        words.zero_()
+        ctx.build_var_dev(data, offs, n, nb, k, words)
+
+    ctx.set_timing(False)
+    for _ in range(max(1, args.warmup // 2)):
+        step()
+    torch.cuda.synchronize(dev)
+    steps = max(1, args.steps // 2)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / steps
+    ctx.set_timing(True)
+    kt = np.zeros(3)
+    for _ in range(steps):
+        words.zero_()
+        ctx.build_var_dev(data, offs, n, nb, k, words)
+        ctx.sync()
+        kt += np.array(ctx.last_build_ms())
+    kt /= steps
+    ctx.set_timing(False)
+    alg = int(data.numel()) + 8 * (n + 1) + 8 * nw
+    res = {"workload": "C4 (configs[3]): %d var-len keys (8-256 B, %.1f B mean) into new(%d, 0.01) (%d bits, k=%d)"
+                       % (n, data.numel() / n, n, nb, k),
+           "value": round(n / dt / 1e6, 1), "unit": "Mkeys/s", "ms_per_step": round(dt * 1e3, 3),
+           "kernel_ms": round(float(kt[0]), 4), "pass_a_ms": round(float(kt[1]), 4),
+           "pass_b_ms": round(float(kt[2]), 4), "algorithmic_bytes": alg,
+           "achieved_GBs": round(alg / (kt[0] * 1e-3) / 1e9, 1),
+           "frac": round(alg / (kt[0] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "strategy": lsmbloom.build_strategy(nb, n)}
+    del data, offs, words
+    torch.cuda.empty_cache()
+    return res
+
+
+def committed_traffic():
+    """HBM bytes per C2 build from the committed rocprofv3 PMC summary
+    (profiles/traffic.json, written by tools/prof_summary.py --json from separate
+    FETCH_SIZE / WRITE_SIZE passes of this bench; FETCH_SIZE doubled per the
+    gfx950 note in MI355X_MICROARCH.md).  None if absent."""
+    p = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(p):
+        return None
+    t = json.load(open(p))
+    return {"bytes": t.get("build_bytes"), "source": "%s (%s)" % (os.path.relpath(p, ROOT), t.get("profile"))}
 
 
 def bench_probe(ctx, dev, args):

@@ -42,7 +42,7 @@ extern "C" {
 #define LSMB_ECORRUPT (-4) /* serialized filter fails validation               */
 #define LSMB_ENOMEM (-5)   /* device or pinned-host allocation failed          */
 
-#define LSMB_ABI_VERSION 2
+#define LSMB_ABI_VERSION 3
 
 typedef struct lsmb_ctx lsmb_ctx; /* one GPU: stream, events, scratch arenas */
 
@@ -106,8 +106,9 @@ void lsmb_close(lsmb_ctx* ctx);
 int lsmb_sync(lsmb_ctx* ctx);
 
 /* ---- batched build (BloomFilterBuilder::add_key loop + build) ------------ */
-/* Host-memory entry points: H2D the keys through pinned staging, build on the
- * GPU, D2H the words (OR-accumulated into `words`).  Synchronous. */
+/* Host-memory entry points: the keys go up in chunks through two device
+ * staging slots (chunk i+1's H2D overlaps chunk i's kernels), the build runs on
+ * the GPU, the words come back (OR-accumulated into `words`).  Synchronous. */
 
 /* n keys of key_len bytes each, packed back to back (key i at keys + i*key_len). */
 int lsmb_build_fixed(lsmb_ctx* ctx, const uint8_t* keys, uint32_t key_len, uint64_t n,
@@ -116,6 +117,21 @@ int lsmb_build_fixed(lsmb_ctx* ctx, const uint8_t* keys, uint32_t key_len, uint6
 /* n variable-length keys: key i = data[offsets[i] .. offsets[i+1]). */
 int lsmb_build_var(lsmb_ctx* ctx, const uint8_t* data, const uint64_t* offsets, uint64_t n,
                    uint32_t num_bits, uint32_t num_hashes, uint64_t* words);
+
+/* The SSTable bloom block in one call: replaces
+ *     let bloom = self.bloom_builder.build();   let bloom_data = bloom.serialize();
+ * of SSTableBuilder::finish (src/sstable/builder.rs:177-179).  Builds a fresh
+ * filter (BloomFilter::new(..) then insert of every key, src/bloom/mod.rs:38-78)
+ * from n host-memory keys — fixed-length (offsets == NULL, key i at
+ * data + i*key_len) or variable-length (key i = data[offsets[i]..offsets[i+1])) —
+ * and writes exactly the bytes BloomFilter::serialize returns
+ * (src/bloom/mod.rs:102-115) into block[0 .. lsmb_serialized_size(num_bits)).
+ * The words go device -> block directly (no host word array, no serialize
+ * copy); the key H2D is chunked and overlapped with the build kernels.
+ * n == 0 gives the empty filter's block.  block_len < the size: LSMB_EINVAL. */
+int lsmb_build_block(lsmb_ctx* ctx, const uint8_t* data, const uint64_t* offsets, uint32_t key_len,
+                     uint64_t n, uint32_t num_bits, uint32_t num_hashes, uint8_t* block,
+                     uint64_t block_len);
 
 /* ---- batched probe (may_contain over a batch of keys x filters) --------- */
 /* For key i and filter f: bit (f % 8) of out_mask[i * ceil(nfilt/8) + f / 8]
@@ -153,6 +169,13 @@ int lsmb_or_reduce_dev(lsmb_ctx* ctx, void* d_dst, const void* d_src, uint64_t n
  * for i in [first, first+n). */
 int lsmb_gen_key16_dev(lsmb_ctx* ctx, uint64_t seed, uint64_t first, uint64_t n, void* d_keys,
                        void* stream);
+
+/* u64 stream: d_out[j] = mod ? add + splitmix64(seed+first+j) % mod
+ *                            : splitmix64(seed+first+j), j in [0, n).
+ * The C4 var-len workload: key lengths (seed 0x5EED0003, mod 249, add 8) and
+ * the packed key bytes (seed 0x5EED0004, mod 0, LE words). */
+int lsmb_gen_splitmix_dev(lsmb_ctx* ctx, uint64_t seed, uint64_t first, uint64_t n, uint32_t mod,
+                          uint32_t add, void* d_out, void* stream);
 
 /* ---- device-resident filter sets (multi-get pre-check) --------------------- */
 /* An lsmb_fset keeps up to 64 SSTable filters resident in device memory, each

@@ -161,6 +161,17 @@ class BloomFilterBuilder {
         }
         return std::move(filter_);
     }
+    // build().serialize() in one GPU call (lsmb_build_block): the bloom block
+    // SSTableBuilder::finish writes (src/sstable/builder.rs:177-179), with the
+    // words copied device -> block directly.
+    std::vector<uint8_t> build_serialized() {
+        std::vector<uint8_t> block(lsmb_serialized_size(filter_.num_bits_));
+        Context& ctx = ctx_ ? *ctx_ : Context::shared();
+        check(lsmb_build_block(ctx.get(), data_.empty() ? nullptr : data_.data(), offsets_.data(), 0,
+                               offsets_.size() - 1, filter_.num_bits_, filter_.num_hashes_, block.data(),
+                               block.size()));
+        return block;
+    }
 
    private:
     BloomFilter filter_;

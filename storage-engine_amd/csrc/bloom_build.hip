@@ -481,6 +481,17 @@ __global__ __launch_bounds__(256) void k_gen_key16(uint64_t seed, uint64_t first
     }
 }
 
+// out[j] = mod ? add + sm(seed + first + j) % mod : sm(seed + first + j)
+// (tests/keygen.py varlen: key lengths with mod 249 / add 8, key bytes with mod 0).
+__global__ __launch_bounds__(256) void k_gen_splitmix(uint64_t seed, uint64_t first, uint64_t n, uint32_t mod,
+                                                      uint32_t add, uint64_t* __restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
+        const uint64_t x = splitmix64(seed + first + j);
+        out[j] = mod ? add + x % mod : x;
+    }
+}
+
 // The max-dynamic-LDS attribute is a property of the kernel, not of a launch:
 // set it once per kernel (to the whole 160 KiB), not before every launch.
 void set_max_lds(const void* fn) {
@@ -668,6 +679,14 @@ hipError_t launch_gen_key16(uint64_t seed, uint64_t first, uint64_t n, uint8_t* 
     if (g > 8192) g = 8192;
     if (g < 1) g = 1;
     k_gen_key16<<<dim3((uint32_t)g), dim3(256), 0, st>>>(seed, first, n, reinterpret_cast<uint4*>(d_keys));
+    return hipGetLastError();
+}
+
+hipError_t launch_gen_splitmix(uint64_t seed, uint64_t first, uint64_t n, uint32_t mod, uint32_t add,
+                               uint64_t* d_out, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    const uint64_t g = std::min<uint64_t>((n + 255) / 256, 8192);
+    k_gen_splitmix<<<dim3((uint32_t)g), dim3(256), 0, st>>>(seed, first, n, mod, add, d_out);
     return hipGetLastError();
 }
 

@@ -102,6 +102,13 @@ struct lsmb_ctx {
     hipEvent_t desc_done = nullptr;          // last kernel that read filt_desc
     std::vector<uint64_t> offs_tmp;
     bool timing = true;            // per-build HIP events (lsmb_set_timing)
+    // host-memory builds: two staging slots, H2D on `cst` overlapping the
+    // kernels of the previous chunk on `st` (host_build)
+    hipStream_t cst = nullptr;
+    hipEvent_t ev_copy[2] = {nullptr, nullptr}, ev_built[2] = {nullptr, nullptr};
+    DevBuf kslot[2], oslot[2];
+    uint64_t* offs_pin[2] = {nullptr, nullptr};  // pinned rebased offsets per slot
+    uint64_t offs_pin_cap[2] = {0, 0};
 };
 
 namespace {
@@ -201,6 +208,92 @@ void for_positions(const uint8_t* key, uint64_t len, uint32_t num_bits, uint32_t
         walk_key<Walk32>(key, len, num_bits, k, f);
     else
         walk_key<Walk64>(key, len, num_bits, k, f);
+}
+
+// offsets[0..n] must be non-decreasing (key i = data[offsets[i] .. offsets[i+1]).
+int check_offsets(const uint64_t* offsets, uint64_t n) {
+    for (uint64_t i = 0; i < n; i++)
+        if (offsets[i + 1] < offsets[i])
+            return fail(LSMB_EINVAL, "offsets not non-decreasing at %llu", (unsigned long long)i);
+    return LSMB_OK;
+}
+
+uint64_t h2d_chunk_bytes() {
+    const char* s = getenv("LSMB_H2D_CHUNK_MB");
+    uint64_t mb = s ? strtoull(s, nullptr, 10) : 128;
+    if (mb < 1) mb = 1;
+    return mb << 20;
+}
+
+// Build from keys in host memory (the flush / compaction path: keys come from a
+// memtable or merge iterator, src/db/mod.rs:379-383).  The keys go up in chunks
+// of <= h2d_chunk_bytes() through two device staging slots: chunk i+1's H2D on
+// the copy stream overlaps chunk i's kernels on the build stream, so the build
+// hides under the PCIe transfer.  words_in == NULL starts from a zeroed filter
+// (BloomFilter::new), else from those words (OR-accumulate); the finished words
+// are copied to words_out (host, any alignment: lsmb_build_block points it at
+// the serialized block body).  Synchronous.
+int host_build(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
+               uint32_t num_bits, uint32_t k, const uint64_t* words_in, uint8_t* words_out) {
+    const uint64_t nw = nwords64(num_bits);
+    HIP_TRY(c->words.ensure(nw * 8));
+    uint32_t* dw = (uint32_t*)c->words.p;
+    if (words_in)
+        HIP_TRY(hipMemcpyAsync(dw, words_in, nw * 8, hipMemcpyHostToDevice, c->st));
+    else
+        HIP_TRY(hipMemsetAsync(dw, 0, nw * 8, c->st));
+    if (!offsets && key_len == 0) {
+        // every key is the empty key: one insert covers them all
+        HIP_TRY(c->kslot[0].ensure(16));
+        KeyBatch kb{(const uint8_t*)c->kslot[0].p, nullptr, 0, 1};
+        if (int rc = build_dev(c, kb, num_bits, k, dw, c->st)) return rc;
+        n = 0;
+    }
+    const uint64_t budget = h2d_chunk_bytes();
+    const uint64_t max_keys = 32ull << 20;  // per chunk (bounds the offsets slot)
+    uint64_t f = 0;
+    for (int i = 0; f < n; i++) {
+        const int s = i & 1;
+        uint64_t e;
+        if (offsets) {  // largest e with offsets[e] - offsets[f] <= budget, at least one key
+            const uint64_t* hi = std::upper_bound(offsets + f + 1, offsets + n + 1, offsets[f] + budget);
+            e = std::max<uint64_t>(f + 1, (uint64_t)(hi - offsets) - 1);
+            e = std::min(e, f + max_keys);
+        } else {
+            e = std::min(n, f + std::max<uint64_t>(1, budget / key_len));
+        }
+        const uint64_t m = e - f;
+        const uint64_t base = offsets ? offsets[f] : f * key_len;
+        const uint64_t bytes = offsets ? offsets[e] - offsets[f] : m * key_len;
+        // slot s was last read by chunk i-2's kernels
+        if (i >= 2) HIP_TRY(hipEventSynchronize(c->ev_built[s]));
+        HIP_TRY(c->kslot[s].ensure(std::max<uint64_t>(bytes, std::min(budget, n * (uint64_t)(key_len ? key_len : 1))) + 16));
+        if (bytes) HIP_TRY(hipMemcpyAsync(c->kslot[s].p, data + base, bytes, hipMemcpyHostToDevice, c->cst));
+        if (offsets) {
+            if (c->offs_pin_cap[s] < m + 1) {
+                if (c->offs_pin[s]) HIP_TRY(hipHostFree(c->offs_pin[s]));
+                c->offs_pin[s] = nullptr;
+                c->offs_pin_cap[s] = 0;
+                const uint64_t cap = std::max<uint64_t>(m + 1, std::min<uint64_t>(n, max_keys) + 1);
+                if (hipHostMalloc((void**)&c->offs_pin[s], cap * 8, 0) != hipSuccess)
+                    return fail(LSMB_ENOMEM, "pinned offsets staging (%llu B)", (unsigned long long)(cap * 8));
+                c->offs_pin_cap[s] = cap;
+            }
+            uint64_t* o = c->offs_pin[s];
+            for (uint64_t j = 0; j <= m; j++) o[j] = offsets[f + j] - base;
+            HIP_TRY(c->oslot[s].ensure(c->offs_pin_cap[s] * 8));
+            HIP_TRY(hipMemcpyAsync(c->oslot[s].p, o, (m + 1) * 8, hipMemcpyHostToDevice, c->cst));
+        }
+        HIP_TRY(hipEventRecord(c->ev_copy[s], c->cst));
+        HIP_TRY(hipStreamWaitEvent(c->st, c->ev_copy[s], 0));
+        KeyBatch kb{(const uint8_t*)c->kslot[s].p, offsets ? (const uint64_t*)c->oslot[s].p : nullptr, key_len, m};
+        if (int rc = build_dev(c, kb, num_bits, k, dw, c->st)) return rc;
+        HIP_TRY(hipEventRecord(c->ev_built[s], c->st));
+        f = e;
+    }
+    HIP_TRY(hipMemcpyAsync(words_out, dw, nw * 8, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    return check_device_error(c);
 }
 
 }  // namespace
@@ -329,7 +422,12 @@ int lsmb_open(lsmb_ctx** out, int device) {
     if (hipStreamCreateWithFlags(&c->st, hipStreamDefault) != hipSuccess ||
         hipEventCreateWithFlags(&c->desc_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreate(&c->tm.t0) != hipSuccess || hipEventCreate(&c->tm.t1) != hipSuccess ||
-        hipEventCreate(&c->tm.t2) != hipSuccess) {
+        hipEventCreate(&c->tm.t2) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->cst, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_copy[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_copy[1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_built[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_built[1], hipEventDisableTiming) != hipSuccess) {
         delete c;
         return fail(LSMB_ENODEV, "stream/event creation failed on device %d", device);
     }
@@ -348,9 +446,16 @@ void lsmb_close(lsmb_ctx* c) {
         DevGuard g(c->dev);
         hipStreamSynchronize(c->st);
         if (c->err_host) hipHostFree(c->err_host);
+        if (c->cst) hipStreamSynchronize(c->cst);
         for (DevBuf* b : {&c->ws_regions, &c->ws_counts, &c->err, &c->keys, &c->offs, &c->words, &c->out,
-                          &c->filt_words, &c->filt_desc})
+                          &c->filt_words, &c->filt_desc, &c->kslot[0], &c->kslot[1], &c->oslot[0], &c->oslot[1]})
             b->release();
+        for (int s = 0; s < 2; s++) {
+            if (c->offs_pin[s]) hipHostFree(c->offs_pin[s]);
+            if (c->ev_copy[s]) hipEventDestroy(c->ev_copy[s]);
+            if (c->ev_built[s]) hipEventDestroy(c->ev_built[s]);
+        }
+        if (c->cst) hipStreamDestroy(c->cst);
         hipEventDestroy(c->tm.t0);
         hipEventDestroy(c->tm.t1);
         hipEventDestroy(c->tm.t2);
@@ -402,23 +507,7 @@ int lsmb_build_fixed(lsmb_ctx* c, const uint8_t* keys, uint32_t key_len, uint64_
     if (!keys && key_len) return fail(LSMB_EINVAL, "null keys");
     if (!words) return fail(LSMB_EINVAL, "null words");
     DevGuard g(c->dev);
-    const uint64_t nw = nwords64(num_bits);
-    HIP_TRY(c->words.ensure(nw * 8));
-    HIP_TRY(hipMemcpyAsync(c->words.p, words, nw * 8, hipMemcpyHostToDevice, c->st));
-    // H2D in chunks of <= 256 MiB of keys.
-    const uint64_t eff_len = key_len ? key_len : 1;
-    const uint64_t per = std::max<uint64_t>(1, (256ull << 20) / eff_len);
-    const uint64_t nn = key_len ? n : 1;  // all-empty keys: one insert
-    HIP_TRY(c->keys.ensure(std::min(per, nn) * eff_len + 16));
-    for (uint64_t f = 0; f < nn; f += per) {
-        const uint64_t m = std::min(per, nn - f);
-        if (key_len) HIP_TRY(hipMemcpyAsync(c->keys.p, keys + f * key_len, m * key_len, hipMemcpyHostToDevice, c->st));
-        KeyBatch kb{(const uint8_t*)c->keys.p, nullptr, key_len, m};
-        if (int rc = build_dev(c, kb, num_bits, k, (uint32_t*)c->words.p, c->st)) return rc;
-    }
-    HIP_TRY(hipMemcpyAsync(words, c->words.p, nw * 8, hipMemcpyDeviceToHost, c->st));
-    HIP_TRY(hipStreamSynchronize(c->st));
-    return check_device_error(c);
+    return host_build(c, keys, nullptr, key_len, n, num_bits, k, words, (uint8_t*)words);
 }
 
 int lsmb_build_var(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, uint64_t n,
@@ -427,32 +516,35 @@ int lsmb_build_var(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, ui
     if (int rc = check_filter(num_bits, k)) return rc;
     if (n == 0 || k == 0) return LSMB_OK;
     if (!offsets || !words) return fail(LSMB_EINVAL, "null pointer");
-    for (uint64_t i = 0; i < n; i++)
-        if (offsets[i + 1] < offsets[i]) return fail(LSMB_EINVAL, "offsets not non-decreasing at %llu", (unsigned long long)i);
+    if (int rc = check_offsets(offsets, n)) return rc;
     DevGuard g(c->dev);
+    return host_build(c, data, offsets, 0, n, num_bits, k, words, (uint8_t*)words);
+}
+
+int lsmb_build_block(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
+                     uint32_t num_bits, uint32_t k, uint8_t* block, uint64_t block_len) {
+    if (!c) return fail(LSMB_EINVAL, "null ctx");
+    if (int rc = check_filter(num_bits, k)) return rc;
     const uint64_t nw = nwords64(num_bits);
-    HIP_TRY(c->words.ensure(nw * 8));
-    HIP_TRY(hipMemcpyAsync(c->words.p, words, nw * 8, hipMemcpyHostToDevice, c->st));
-    const uint64_t budget = 256ull << 20;  // bytes of key data per chunk
-    uint64_t f = 0;
-    while (f < n) {
-        uint64_t e = f + 1;  // at least one key (a single key may exceed the budget)
-        while (e < n && offsets[e + 1] - offsets[f] <= budget && e - f < (32ull << 20)) e++;
-        const uint64_t bytes = offsets[e] - offsets[f];
-        HIP_TRY(c->keys.ensure(bytes + 16));
-        HIP_TRY(c->offs.ensure((e - f + 1) * 8));
-        c->offs_tmp.resize(e - f + 1);
-        for (uint64_t i = f; i <= e; i++) c->offs_tmp[i - f] = offsets[i] - offsets[f];
-        if (bytes) HIP_TRY(hipMemcpyAsync(c->keys.p, data + offsets[f], bytes, hipMemcpyHostToDevice, c->st));
-        HIP_TRY(hipMemcpyAsync(c->offs.p, c->offs_tmp.data(), (e - f + 1) * 8, hipMemcpyHostToDevice, c->st));
-        KeyBatch kb{(const uint8_t*)c->keys.p, (const uint64_t*)c->offs.p, 0, e - f};
-        if (int rc = build_dev(c, kb, num_bits, k, (uint32_t*)c->words.p, c->st)) return rc;
-        HIP_TRY(hipStreamSynchronize(c->st));  // offs_tmp is reused by the next chunk
-        f = e;
+    const uint64_t size = 12 + 8 * nw;
+    if (!block) return fail(LSMB_EINVAL, "null block");
+    if (block_len < size)
+        return fail(LSMB_EINVAL, "block buffer %llu B < serialized size %llu B", (unsigned long long)block_len,
+                    (unsigned long long)size);
+    if (n && !offsets && !data && key_len) return fail(LSMB_EINVAL, "null keys");
+    if (n && offsets) {
+        if (int rc = check_offsets(offsets, n)) return rc;
     }
-    HIP_TRY(hipMemcpyAsync(words, c->words.p, nw * 8, hipMemcpyDeviceToHost, c->st));
-    HIP_TRY(hipStreamSynchronize(c->st));
-    return check_device_error(c);
+    // header of BloomFilter::serialize (src/bloom/mod.rs:102-115)
+    const uint32_t hdr[3] = {k, num_bits, (uint32_t)nw};
+    for (int i = 0; i < 3; i++)
+        for (int b = 0; b < 4; b++) block[4 * i + b] = (uint8_t)(hdr[i] >> (8 * b));
+    if (n == 0 || k == 0) {  // new() + no inserts: all-zero words
+        memset(block + 12, 0, nw * 8);
+        return LSMB_OK;
+    }
+    DevGuard g(c->dev);
+    return host_build(c, data, offsets, key_len, n, num_bits, k, nullptr, block + 12);
 }
 
 // Copies a host key batch into the context's staging buffers (ctx stream).
@@ -566,6 +658,16 @@ int lsmb_or_reduce_dev(lsmb_ctx* c, void* dst, const void* src, uint64_t nwords,
     DevGuard g(c->dev);
     HIP_TRY(launch_or_reduce((uint32_t*)dst, (const uint32_t*)src, 2 * nwords, nsrc, 2 * stride_words,
                              pick_stream(c, stream)));
+    return LSMB_OK;
+}
+
+int lsmb_gen_splitmix_dev(lsmb_ctx* c, uint64_t seed, uint64_t first, uint64_t n, uint32_t mod, uint32_t add,
+                          void* d_out, void* stream) {
+    if (!c) return fail(LSMB_EINVAL, "null ctx");
+    if (n && !d_out) return fail(LSMB_EINVAL, "null device pointer");
+    if (((uintptr_t)d_out) & 7) return fail(LSMB_EINVAL, "d_out must be 8-byte aligned");
+    DevGuard g(c->dev);
+    HIP_TRY(launch_gen_splitmix(seed, first, n, mod, add, (uint64_t*)d_out, pick_stream(c, stream)));
     return LSMB_OK;
 }
 

@@ -108,6 +108,8 @@ hipError_t launch_probe(const KeyBatch& kb, const ProbeFilter* h_filters, uint32
 hipError_t launch_or_reduce(uint32_t* dst, const uint32_t* src, uint64_t nwords32, uint32_t nsrc,
                             uint64_t stride32, hipStream_t st);
 
+hipError_t launch_gen_splitmix(uint64_t seed, uint64_t first, uint64_t n, uint32_t mod, uint32_t add,
+                               uint64_t* d_out, hipStream_t st);
 hipError_t launch_gen_key16(uint64_t seed, uint64_t first, uint64_t n, uint8_t* d_keys,
                             hipStream_t st);
 

@@ -52,6 +52,8 @@ SIGNATURES = {
     "lsmb_build_fixed": (ctypes.c_int, [vp, u8p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
                                         ctypes.c_uint32, u64p]),
     "lsmb_build_var": (ctypes.c_int, [vp, u8p, u64p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, u64p]),
+    "lsmb_build_block": (ctypes.c_int, [vp, u8p, u64p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
+                                        ctypes.c_uint32, u8p, ctypes.c_uint64]),
     "lsmb_probe": (ctypes.c_int, [vp, ctypes.POINTER(u64p), u32p, u32p, ctypes.c_uint32, u8p, u64p,
                                   ctypes.c_uint32, ctypes.c_uint64, u8p]),
     "lsmb_build_fixed_dev": (ctypes.c_int, [vp, vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
@@ -62,6 +64,8 @@ SIGNATURES = {
                                       ctypes.c_uint32, ctypes.c_uint64, vp, vp]),
     "lsmb_or_reduce_dev": (ctypes.c_int, [vp, vp, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, vp]),
     "lsmb_gen_key16_dev": (ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, vp, vp]),
+    "lsmb_gen_splitmix_dev": (ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                             ctypes.c_uint32, vp, vp]),
     "lsmb_fset_open": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
     "lsmb_fset_close": (None, [vp]),
     "lsmb_fset_add": (ctypes.c_int, [vp, u8p, ctypes.c_uint64, u8p, ctypes.c_uint64, u8p, ctypes.c_uint64]),
@@ -146,6 +150,10 @@ def num_words(num_bits):
     return int(lib().lsmb_num_words(num_bits))
 
 
+def serialized_size(num_bits):
+    return int(lib().lsmb_serialized_size(num_bits))
+
+
 def positions(key, num_bits, k):
     a, n = _key(key)
     out = np.zeros(max(k, 1), dtype=np.uint32)
@@ -197,6 +205,27 @@ class Context:
         _check(lib().lsmb_build_var(self.h, _p(data, u8p), _p(offsets, u64p), offsets.size - 1, num_bits, k,
                                     _p(words, u64p)))
         return words
+
+    def build_block(self, data, num_bits, k, offsets=None, key_len=0, out=None):
+        """The serialized bloom block (BloomFilter::serialize of a fresh filter over
+        the keys, src/bloom/mod.rs:102-115) in one call: lsmb_build_block.  Keys are
+        fixed-length (key_len) or var-length (offsets, n+1 u64).  `out` may be a
+        preallocated uint8 array (e.g. the SST write buffer); returns the array."""
+        data = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+        if offsets is not None:
+            offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+            n = offsets.size - 1
+            op = _p(offsets, u64p)
+        else:
+            n = data.size // key_len if key_len else 0
+            op = None
+        size = serialized_size(num_bits)
+        if out is None:
+            out = np.empty(size, dtype=np.uint8)
+        if data.size == 0:
+            data = np.zeros(1, np.uint8)
+        _check(lib().lsmb_build_block(self.h, _p(data, u8p), op, key_len, n, num_bits, k, _p(out, u8p), out.size))
+        return out
 
     def probe(self, filters, data, offsets=None, key_len=0):
         """filters: [(words uint64 array, num_bits, k)] -> uint8 [n, ceil(F/8)] mask."""
@@ -252,6 +281,26 @@ class Context:
 
     def gen_key16_dev(self, seed, first, n, out, stream=None):
         _check(lib().lsmb_gen_key16_dev(self.h, seed, first, n, vp(out.data_ptr()), self._stream(stream)))
+
+    def gen_splitmix_dev(self, seed, first, n, out, mod=0, add=0, stream=None):
+        _check(lib().lsmb_gen_splitmix_dev(self.h, seed, first, n, mod, add, out.data_ptr(), self._stream(stream)))
+
+    def gen_varlen_dev(self, n, first=0, device=None):
+        """C4 keys [first, first+n) of tests/keygen.varlen on the device ->
+        (data uint8 tensor, offsets int64 tensor [n+1], rebased to 0)."""
+        import torch
+        dev = device or torch.device("cuda", torch.cuda.current_device())
+        lens = torch.empty(first + n, dtype=torch.int64, device=dev)
+        self.gen_splitmix_dev(0x5EED0003, 0, first + n, lens, mod=249, add=8)
+        offs = torch.zeros(first + n + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(lens, 0, out=offs[1:])
+        del lens
+        o0, o1 = int(offs[first].item()), int(offs[first + n].item())
+        w0, w1 = o0 // 8, (o1 + 7) // 8
+        words = torch.empty(max(w1 - w0, 1), dtype=torch.int64, device=dev)
+        self.gen_splitmix_dev(0x5EED0004, w0, w1 - w0, words)
+        data = words.view(torch.uint8)[o0 - 8 * w0: o0 - 8 * w0 + (o1 - o0)]
+        return data, (offs[first:] - o0).contiguous()
 
     def set_timing(self, on):
         """Per-build HIP events (lsmb_last_build_ms) on/off."""
@@ -441,3 +490,12 @@ class BloomFilterBuilder:
             data = np.frombuffer(bytes(self._data), dtype=np.uint8)
             ctx.build_var(data, offs, f._nb, f._k, f.bits)
         return f
+
+    def build_serialized(self):
+        """build().serialize() in one GPU call (lsmb_build_block): the bloom block
+        SSTableBuilder::finish writes (src/sstable/builder.rs:177-179)."""
+        f = self._filter
+        ctx = self._ctx or default_context()
+        offs = np.array(self._offs, dtype=np.uint64)
+        data = np.frombuffer(bytes(self._data), dtype=np.uint8)
+        return ctx.build_block(data, f._nb, f._k, offsets=offs).tobytes()

@@ -17,6 +17,30 @@ def short(name):
     return n[:90]
 
 
+def traffic_json(d, out):
+    """Per-dispatch HBM bytes of the C2 build kernels (k_bin<Fixed16...> +
+    k_apply) -> JSON read by bench.py (roofline.traffic)."""
+    import json
+    per = collections.defaultdict(dict)
+    for sub, cn in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+        p = os.path.join(d, sub, "run_counter_collection.csv")
+        vals = collections.defaultdict(list)
+        for r in csv.DictReader(open(p)):
+            if r["Counter_Name"] == cn:
+                vals[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+        for kn, v in vals.items():
+            per[kn][cn] = sum(v) / len(v)
+    kern = {}
+    for kn, m in per.items():
+        if kn.startswith("k_bin<ks::Fixed16") or kn == "k_apply":
+            kern[kn] = {"read_bytes": int(2 * m.get("FETCH_SIZE", 0) * 1024),
+                        "write_bytes": int(m.get("WRITE_SIZE", 0) * 1024)}
+    tot = sum(v["read_bytes"] + v["write_bytes"] for v in kern.values())
+    json.dump({"profile": os.path.basename(d.rstrip("/")), "build_bytes": tot, "kernels": kern,
+               "note": "FETCH_SIZE x2 (gfx950), KiB -> B; mean per dispatch over separate --pmc passes"},
+              open(out, "w"), indent=1)
+
+
 def main(d):
     print("# rocprofv3 summary: %s\n" % os.path.basename(d.rstrip("/")))
     ks = os.path.join(d, "stats", "run_kernel_stats.csv")
@@ -53,4 +77,7 @@ def main(d):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    if len(sys.argv) > 3 and sys.argv[2] == "--json":
+        traffic_json(sys.argv[1], sys.argv[3])
+    else:
+        main(sys.argv[1])
