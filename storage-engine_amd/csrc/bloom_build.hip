@@ -30,8 +30,11 @@
 #include <mutex>
 #include <vector>
 
+#include <type_traits>
+
 #include "kernels.hpp"
 #include "keysrc.hpp"
+#include "hash_var.hpp"
 
 // LSMB_ABL (timing ablations for tools/, never in the product build):
 //   1 = no segment flush, 2 = no claims/stores, 8 = no region stores,
@@ -49,6 +52,7 @@ namespace {
 using ks::Fixed16;
 using ks::FixedN;
 using ks::VarLen;
+using ks::Hashed;
 
 __device__ __forceinline__ void or_bit_global(uint32_t* w, uint32_t p) {
     atomicOr(w + (p >> 5), 1u << (p & 31));
@@ -492,6 +496,17 @@ __global__ __launch_bounds__(256) void k_gen_splitmix(uint64_t seed, uint64_t fi
     }
 }
 
+// (h1, h2) = xxh3_128(key i) for every key, as 16-B records (ks::Hashed).
+// Full occupancy and no barriers, so the per-lane key-byte loads of many
+// waves overlap; pass A then reads 16 coalesced bytes per key.
+template <class Src>
+__global__ __launch_bounds__(256) void k_hash(Src src, uint64_t n, uint4* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const H128 h = src.hash(i);
+    out[i] = make_uint4((uint32_t)h.lo, (uint32_t)(h.lo >> 32), (uint32_t)h.hi, (uint32_t)(h.hi >> 32));
+}
+
 // The max-dynamic-LDS attribute is a property of the kernel, not of a launch:
 // set it once per kernel (to the whole 160 KiB), not before every launch.
 void set_max_lds(const void* fn) {
@@ -507,10 +522,10 @@ void set_max_lds(const void* fn) {
 template <class Src>
 hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k, uint32_t* gw,
                       BuildStrategy s, const PartitionWorkspace& ws, int num_cus, hipStream_t st,
-                      BuildTimers* tm) {
+                      BuildTimers* tm, bool t0_done = false) {
     const Mod32 md = Mod32::make(num_bits);
     const uint32_t nw32 = (uint32_t)(2 * (((uint64_t)num_bits + 63) / 64));
-    if (tm) hipEventRecord(tm->t0, st);
+    if (tm && !t0_done) hipEventRecord(tm->t0, st);
     if (s == BuildStrategy::Lds) {
         const size_t smem = (size_t)nw32 * 4;
         // ~8 Ki keys per workgroup keeps the final per-word OR cheap.
@@ -526,6 +541,16 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
         if (g > (uint64_t)num_cus * 8) g = (uint64_t)num_cus * 8;
         k_build_atomic<Src><<<dim3((uint32_t)g), dim3(256), 0, st>>>(src, n, md, k, gw);
         if (tm) hipEventRecord(tm->t1, st);
+    } else if constexpr (Src::kPrehash) {
+        if (ws.hash_bytes < n * 16) return hipErrorInvalidValue;
+        const uint64_t g = (n + 255) / 256;
+        if (g > 0x7FFFFFFFull) return hipErrorInvalidValue;
+        if constexpr (std::is_same<Src, VarLen>::value)
+            k_hash_var<0><<<dim3((uint32_t)g), dim3(256), 0, st>>>(src.d, src.o, n, ws.hashes);
+        else
+            k_hash<Src><<<dim3((uint32_t)g), dim3(256), 0, st>>>(src, n, ws.hashes);
+        // pass A's timer (t1) covers k_hash + k_bin
+        return build_with(Hashed{ws.hashes}, n, num_bits, k, gw, s, ws, num_cus, st, tm, /*t0_done=*/true);
     } else {
         const PartitionPlan pl = plan_partition(num_bits, k, n, num_cus);
         if (pl.region_bytes > ws.region_bytes || pl.counts_bytes > ws.counts_bytes) return hipErrorInvalidValue;

@@ -91,6 +91,7 @@ struct lsmb_ctx {
     hipStream_t st = nullptr;
     BuildTimers tm;
     DevBuf ws_regions, ws_counts;  // partition workspace
+    DevBuf ws_hashes;              // partition workspace: k_hash records (var-len / odd-length keys)
     DevBuf err;                    // device error flag of the partition kernels
     uint32_t* err_host = nullptr;  // pinned mirror read at sync
     DevBuf keys, offs, words, out; // staging for the host-memory entry points
@@ -178,6 +179,12 @@ int build_dev(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k
     ws.err = (uint32_t*)c->err.p;
     ws.region_bytes = c->ws_regions.bytes;
     ws.counts_bytes = c->ws_counts.bytes;
+    const bool fixed16 = !kb_all.offsets && kb_all.key_len == 16 && (reinterpret_cast<uintptr_t>(kb_all.data) & 15) == 0;
+    if (!fixed16) {  // pre-hashed pass A (ks::Hashed): 16 B per key of the chunk
+        HIP_TRY(c->ws_hashes.ensure(chunk * 16));
+        ws.hashes = (uint4*)c->ws_hashes.p;
+        ws.hash_bytes = c->ws_hashes.bytes;
+    }
     for (uint64_t first = 0; first < kb_all.n; first += chunk) {
         KeyBatch kb = kb_all;
         kb.n = std::min(chunk, kb_all.n - first);
@@ -447,7 +454,7 @@ void lsmb_close(lsmb_ctx* c) {
         hipStreamSynchronize(c->st);
         if (c->err_host) hipHostFree(c->err_host);
         if (c->cst) hipStreamSynchronize(c->cst);
-        for (DevBuf* b : {&c->ws_regions, &c->ws_counts, &c->err, &c->keys, &c->offs, &c->words, &c->out,
+        for (DevBuf* b : {&c->ws_regions, &c->ws_counts, &c->ws_hashes, &c->err, &c->keys, &c->offs, &c->words, &c->out,
                           &c->filt_words, &c->filt_desc, &c->kslot[0], &c->kslot[1], &c->oslot[0], &c->oslot[1]})
             b->release();
         for (int s = 0; s < 2; s++) {

@@ -1,0 +1,120 @@
+// hash_var.hpp — k_hash_var: XXH3-128 of packed variable-length keys through
+// an LDS window (device side, internal; included by bloom_build.hip and
+// tools/mb_varhash.hip).
+#pragma once
+
+#include "keysrc.hpp"
+
+namespace lsmb {
+
+// Key bytes from a workgroup's LDS window (k_hash_var): LE loads at any byte
+// offset as funnel shifts of aligned dwords (the window has >= 12 B of slack).
+struct LdsReader {
+    const uint32_t* w;
+    uint32_t base;  // the key's first byte in the window
+    __device__ __forceinline__ uint64_t ld64(uint64_t o) const {
+        const uint32_t a = base + (uint32_t)o, i = a >> 2, sh = (a & 3) * 8;
+        const uint32_t d0 = w[i], d1 = w[i + 1], d2 = w[i + 2];
+        return ((uint64_t)__builtin_amdgcn_alignbit(d2, d1, sh) << 32) | __builtin_amdgcn_alignbit(d1, d0, sh);
+    }
+    __device__ __forceinline__ uint32_t ld32(uint64_t o) const {
+        const uint32_t a = base + (uint32_t)o, i = a >> 2, sh = (a & 3) * 8;
+        return __builtin_amdgcn_alignbit(w[i + 1], w[i], sh);
+    }
+    __device__ __forceinline__ uint32_t u8(uint64_t o) const {
+        const uint32_t a = base + (uint32_t)o;
+        return (w[a >> 2] >> ((a & 3) * 8)) & 0xFFu;
+    }
+};
+
+// k_hash for packed variable-length keys.  A workgroup's 256 keys are one
+// contiguous byte range (C4: ~34 KB).  It is staged into LDS with coalesced,
+// aligned 16-B loads — all of a thread's loads issued before its first LDS
+// write, so ~10 KB per wave are in flight — and every lane hashes a key from
+// LDS.  Per-lane reads straight from HBM touch a different cache line per
+// lane per load.  Lanes are assigned to keys by length class (a counting sort
+// of the 256 keys by ceil(len/32)), so a wave runs one XXH3 length path
+// instead of all of them: mixed 8-256 B keys cost the divergent sum of the
+// 0-16 / 17-128 / 129-240 / long paths otherwise (tools/mb_varhash.hip).
+// Keys that do not fit the window start another round at the first unhashed
+// key; a key longer than the whole window is hashed from global memory.
+constexpr uint32_t kHashWin = 40 * 1024;
+constexpr uint32_t kHashPieces = kHashWin / (256 * 16);  // 16-B loads per thread per round
+
+__device__ __forceinline__ uint32_t len_class(uint64_t len) {
+    if (len <= 16) return 0;
+    if (len <= 240) return 1 + (uint32_t)((len - 1) >> 5);  // 1..8: the 17-128 / 129-240 round counts
+    return 9;
+}
+
+template <int MODE = 0>
+__global__ __launch_bounds__(256) void k_hash_var(const uint8_t* __restrict__ d, const uint64_t* __restrict__ o,
+                                                  uint64_t n, uint4* __restrict__ out) {
+    __shared__ uint32_t win[kHashWin / 4 + 8];
+    __shared__ uint64_t ks_a[256], ks_b[256];
+    __shared__ uint32_t cls_cnt[16];
+    __shared__ uint16_t perm[256];
+    const uint32_t t = threadIdx.x;
+    const uint64_t i0 = (uint64_t)blockIdx.x * 256;
+    const uint32_t m = (uint32_t)min<uint64_t>(256, n - i0);
+    // key offsets to LDS; lane assignment by length class
+    uint64_t a0 = 0, b0 = 0;
+    if (t < m) {
+        a0 = o[i0 + t];
+        b0 = o[i0 + t + 1];
+    }
+    ks_a[t] = a0;
+    ks_b[t] = b0;
+    if (t < 16) cls_cnt[t] = 0;
+    __syncthreads();
+    const uint32_t cls = t < m ? len_class(b0 - a0) : 15;
+    const uint32_t rank = atomicAdd(&cls_cnt[cls], 1u);
+    __syncthreads();
+    uint32_t base = 0;
+    for (uint32_t c = 0; c < cls; c++) base += cls_cnt[c];
+    perm[base + rank] = (uint16_t)t;
+    __syncthreads();
+    const uint32_t j = perm[t];  // the key this lane hashes
+    const uint64_t ka = ks_a[j], kb = ks_b[j];
+    const uintptr_t end = (uintptr_t)(d + o[i0 + m]);  // one past the last key byte
+    const uintptr_t pa = (uintptr_t)(d + ka), pb = (uintptr_t)(d + kb);
+    H128 h{0, 0};
+    uint32_t f = 0;  // first key not hashed yet (uniform)
+    while (f < m) {
+        // Window [A, wend): A = the 16-B block holding key f's first byte.
+        // Every 16-B piece loaded holds at least one key byte, so no load
+        // leaves the data's pages.
+        const uintptr_t A = (uintptr_t)(d + ks_a[f]) & ~(uintptr_t)15;
+        const uintptr_t wend = min(A + (uintptr_t)kHashWin, end);
+        const uint32_t nb = (uint32_t)(wend - A);
+        uint4 v[kHashPieces];
+#pragma unroll
+        for (uint32_t r = 0; r < kHashPieces; r++) {
+            const uint32_t q = (r * 256 + t) * 16;
+            v[r] = q < nb ? ld_stream16((const uint4*)(A + q)) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (uint32_t r = 0; r < kHashPieces; r++) {
+            const uint32_t q = (r * 256 + t) * 16;
+            if (q < nb) *(uint4*)((char*)win + q) = v[r];
+        }
+        __syncthreads();
+        // keys f.. that end inside the window: a prefix (offsets ascend)
+        const bool fits = j >= f && j < m && pb <= wend;
+        if (MODE == 1) {  // microbenchmark: staging only
+            if (fits) h.lo ^= win[(pa - A) >> 2];
+        } else if (fits) {
+            h = xxh3_128_r(LdsReader{win, (uint32_t)(pa - A)}, kb - ka);
+        }
+        const uint32_t c = (uint32_t)__syncthreads_count(fits);
+        if (c == 0) {  // key f alone is longer than the window
+            if (j == f) h = xxh3_128(d + ka, kb - ka);
+            f++;
+        } else {
+            f += c;
+        }
+    }
+    if (j < m) out[i0 + j] = make_uint4((uint32_t)h.lo, (uint32_t)(h.lo >> 32), (uint32_t)h.hi, (uint32_t)(h.hi >> 32));
+}
+
+}  // namespace lsmb

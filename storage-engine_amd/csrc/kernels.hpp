@@ -58,6 +58,8 @@ PartitionPlan plan_partition(uint32_t num_bits, uint32_t k, uint64_t n, int num_
 uint64_t partition_chunk_keys(uint32_t num_bits, uint32_t k, uint64_t max_bytes, int num_cus);
 
 struct PartitionWorkspace {
+    uint4* hashes = nullptr;  // 16 B per key: k_hash output for var-len / odd-length keys
+    uint64_t hash_bytes = 0;
     uint64_t* regions = nullptr;
     uint32_t* counts = nullptr;
     uint32_t* err = nullptr;  // device flag, see PassA::err

@@ -18,6 +18,7 @@ namespace ks {
 // 16-byte keys on a 16-byte-aligned base: one dwordx4 load per key, streamed
 // past the caches (each key is read exactly once).
 struct Fixed16 {
+    static constexpr bool kPrehash = false;  // hashed inline by pass A
     const uint4* k;
     __device__ __forceinline__ H128 hash(uint64_t i) const {
         uint4 v = ld_stream16(k + i);
@@ -37,6 +38,7 @@ struct Fixed16 {
 
 // Any fixed key length, any alignment.
 struct FixedN {
+    static constexpr bool kPrehash = true;  // partitioned builds hash in k_hash first
     const uint8_t* d;
     uint32_t len;
     __device__ __forceinline__ H128 hash(uint64_t i) const { return xxh3_128(d + i * len, len); }
@@ -49,6 +51,7 @@ struct FixedN {
 
 // Packed variable-length keys: key i = d[o[i] .. o[i+1]).
 struct VarLen {
+    static constexpr bool kPrehash = true;  // partitioned builds hash in k_hash first
     const uint8_t* d;
     const uint64_t* o;
     __device__ __forceinline__ H128 hash(uint64_t i) const {
@@ -63,6 +66,24 @@ struct VarLen {
     };
     __device__ __forceinline__ Pre fetch(uint64_t i, bool ok) const { return ok ? Pre{o[i], o[i + 1]} : Pre{0, 0}; }
     __device__ __forceinline__ H128 hash_pre(const Pre& p, uint64_t) const { return xxh3_128(d + p.a, p.b - p.a); }
+};
+
+// Keys already hashed by k_hash: (h1, h2) of key i as one 16-B record, read
+// with one coalesced dwordx4 like Fixed16.  Pass A over variable-length keys
+// runs on these: its phase-synchronous loop (one key per lane per phase,
+// barriers between phases, one workgroup per CU) would otherwise expose the
+// latency of every key-byte load and the length-class divergence of XXH3.
+struct Hashed {
+    static constexpr bool kPrehash = false;
+    const uint4* h;
+    __device__ __forceinline__ H128 hash(uint64_t i) const { return hash_pre(ld_stream16(h + i), i); }
+    using Pre = uint4;
+    __device__ __forceinline__ Pre fetch(uint64_t i, bool ok) const {
+        return ok ? ld_stream16(h + i) : make_uint4(0, 0, 0, 0);
+    }
+    __device__ __forceinline__ H128 hash_pre(const Pre& v, uint64_t) const {
+        return H128{((uint64_t)v.y << 32) | v.x, ((uint64_t)v.w << 32) | v.z};
+    }
 };
 
 }  // namespace ks

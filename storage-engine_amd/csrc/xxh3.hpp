@@ -122,8 +122,20 @@ LSMB_HD H128 len0() {
     return H128{aval64(a), aval64(b)};
 }
 
-LSMB_HD H128 len1to3(const uint8_t* p, uint32_t len) {
-    uint32_t c1 = p[0], c2 = p[len >> 1], c3 = p[len - 1];
+// Key bytes are read through a Reader (r.ld64(o) / r.ld32(o) / r.u8(o): LE
+// loads at byte offset o of the key): PtrReader for memory the lane addresses
+// directly, or a kernel's LDS window (k_hash_var) — one implementation of
+// every length class for both.
+struct PtrReader {
+    const uint8_t* p;
+    LSMB_HD uint64_t ld64(uint64_t o) const { return xx::ld64(p + o); }
+    LSMB_HD uint32_t ld32(uint64_t o) const { return xx::ld32(p + o); }
+    LSMB_HD uint32_t u8(uint64_t o) const { return p[o]; }
+};
+
+template <class R>
+LSMB_HD H128 len1to3(const R& r, uint32_t len) {
+    uint32_t c1 = r.u8(0), c2 = r.u8(len >> 1), c3 = r.u8(len - 1);
     uint32_t cl = (c1 << 16) | (c2 << 24) | c3 | (len << 8);
     uint32_t ch = rotl32(bswap32(cl), 13);
     constexpr uint64_t fl = (uint64_t)(sec32(0) ^ sec32(4));
@@ -131,8 +143,9 @@ LSMB_HD H128 len1to3(const uint8_t* p, uint32_t len) {
     return H128{aval64((uint64_t)cl ^ fl), aval64((uint64_t)ch ^ fh)};
 }
 
-LSMB_HD H128 len4to8(const uint8_t* p, uint32_t len) {
-    uint64_t v = (uint64_t)ld32(p) | ((uint64_t)ld32(p + len - 4) << 32);
+template <class R>
+LSMB_HD H128 len4to8(const R& r, uint32_t len) {
+    uint64_t v = (uint64_t)r.ld32(0) | ((uint64_t)r.ld32(len - 4) << 32);
     constexpr uint64_t flip = sec64(16) ^ sec64(24);
     H128 m = mul128(v ^ flip, P64_1 + ((uint64_t)len << 2));
     m.hi += m.lo << 1;
@@ -144,8 +157,9 @@ LSMB_HD H128 len4to8(const uint8_t* p, uint32_t len) {
     return m;
 }
 
-LSMB_HD void mix32(H128& acc, const uint8_t* a, const uint8_t* b, int so) {
-    uint64_t a0 = ld64(a), a1 = ld64(a + 8), b0 = ld64(b), b1 = ld64(b + 8);
+template <class R>
+LSMB_HD void mix32(H128& acc, const R& r, uint64_t a, uint64_t b, int so) {
+    uint64_t a0 = r.ld64(a), a1 = r.ld64(a + 8), b0 = r.ld64(b), b1 = r.ld64(b + 8);
     acc.lo += fold(a0 ^ sec64(so), a1 ^ sec64(so + 8));
     acc.lo ^= b0 + b1;
     acc.hi += fold(b0 ^ sec64(so + 16), b1 ^ sec64(so + 24));
@@ -158,35 +172,38 @@ LSMB_HD H128 mid_finish(H128 acc, uint64_t len) {
     return H128{aval3(lo), 0 - aval3(hi)};
 }
 
-LSMB_HD H128 len17to128(const uint8_t* p, uint32_t len) {
+template <class R>
+LSMB_HD H128 len17to128(const R& r, uint32_t len) {
     H128 acc{(uint64_t)len * P64_1, 0};
     if (len > 32) {
         if (len > 64) {
-            if (len > 96) mix32(acc, p + 48, p + len - 64, 96);
-            mix32(acc, p + 32, p + len - 48, 64);
+            if (len > 96) mix32(acc, r, 48, len - 64, 96);
+            mix32(acc, r, 32, len - 48, 64);
         }
-        mix32(acc, p + 16, p + len - 32, 32);
+        mix32(acc, r, 16, len - 32, 32);
     }
-    mix32(acc, p, p + len - 16, 0);
+    mix32(acc, r, 0, len - 16, 0);
     return mid_finish(acc, len);
 }
 
-LSMB_HD H128 len129to240(const uint8_t* p, uint32_t len) {
+template <class R>
+LSMB_HD H128 len129to240(const R& r, uint32_t len) {
     H128 acc{(uint64_t)len * P64_1, 0};
 #pragma unroll
-    for (int i = 0; i < 4; i++) mix32(acc, p + 32 * i, p + 32 * i + 16, 32 * i);
+    for (int i = 0; i < 4; i++) mix32(acc, r, 32 * i, 32 * i + 16, 32 * i);
     acc.lo = aval3(acc.lo);
     acc.hi = aval3(acc.hi);
     const uint32_t rounds = len >> 5;
-    for (uint32_t i = 4; i < rounds; i++) mix32(acc, p + 32 * i, p + 32 * i + 16, 3 + 32 * (int)(i - 4));
-    mix32(acc, p + len - 16, p + len - 32, 136 - 17 - 16);
+    for (uint32_t i = 4; i < rounds; i++) mix32(acc, r, 32 * i, 32 * i + 16, 3 + 32 * (int)(i - 4));
+    mix32(acc, r, len - 16, len - 32, 136 - 17 - 16);
     return mid_finish(acc, len);
 }
 
-LSMB_HD void stripe(uint64_t acc[8], const uint8_t* p, int so) {
+template <class R>
+LSMB_HD void stripe(uint64_t acc[8], const R& r, uint64_t o, int so) {
 #pragma unroll
     for (int i = 0; i < 8; i++) {
-        uint64_t v = ld64(p + 8 * i);
+        uint64_t v = r.ld64(o + 8 * i);
         uint64_t k = v ^ sec64(so + 8 * i);
         acc[i ^ 1] += v;
         acc[i] += (uint64_t)(uint32_t)k * (k >> 32);
@@ -202,12 +219,12 @@ LSMB_HD uint64_t merge(const uint64_t acc[8], int so, uint64_t start) {
 }
 
 // len > 240: 1 KiB blocks of 16 stripes + scramble, then the tail stripes.
-LSMB_HD H128 hash_long(const uint8_t* p, uint64_t len) {
+template <class R>
+LSMB_HD H128 hash_long(const R& r, uint64_t len) {
     uint64_t acc[8] = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1};
     const uint64_t nblocks = (len - 1) >> 10;
     for (uint64_t b = 0; b < nblocks; b++) {
-        const uint8_t* blk = p + (b << 10);
-        for (int s = 0; s < 16; s++) stripe(acc, blk + 64 * s, 8 * s);
+        for (int s = 0; s < 16; s++) stripe(acc, r, (b << 10) + 64 * s, 8 * s);
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             uint64_t a = acc[i];
@@ -216,27 +233,31 @@ LSMB_HD H128 hash_long(const uint8_t* p, uint64_t len) {
             acc[i] = a * P32_1;
         }
     }
-    const uint8_t* last = p + (nblocks << 10);
+    const uint64_t last = nblocks << 10;
     const int nstripes = (int)(((len - 1) - (nblocks << 10)) >> 6);
-    for (int s = 0; s < nstripes; s++) stripe(acc, last + 64 * s, 8 * s);
-    stripe(acc, p + len - 64, 192 - 64 - 7);
+    for (int s = 0; s < nstripes; s++) stripe(acc, r, last + 64 * s, 8 * s);
+    stripe(acc, r, len - 64, 192 - 64 - 7);
     return H128{merge(acc, 11, len * P64_1), merge(acc, 192 - 64 - 11, ~(len * P64_2))};
 }
 
 }  // namespace xx
 
-// XXH3-128 of an arbitrary key.
-LSMB_HD H128 xxh3_128(const uint8_t* p, uint64_t len) {
+// XXH3-128 of an arbitrary key read through `r` (see xx::PtrReader).
+template <class R>
+LSMB_HD H128 xxh3_128_r(const R& r, uint64_t len) {
     if (len <= 16) {
-        if (len > 8) return xx::len9to16(xx::ld64(p), xx::ld64(p + len - 8), len);
-        if (len >= 4) return xx::len4to8(p, (uint32_t)len);
-        if (len) return xx::len1to3(p, (uint32_t)len);
+        if (len > 8) return xx::len9to16(r.ld64(0), r.ld64(len - 8), len);
+        if (len >= 4) return xx::len4to8(r, (uint32_t)len);
+        if (len) return xx::len1to3(r, (uint32_t)len);
         return xx::len0();
     }
-    if (len <= 128) return xx::len17to128(p, (uint32_t)len);
-    if (len <= 240) return xx::len129to240(p, (uint32_t)len);
-    return xx::hash_long(p, len);
+    if (len <= 128) return xx::len17to128(r, (uint32_t)len);
+    if (len <= 240) return xx::len129to240(r, (uint32_t)len);
+    return xx::hash_long(r, len);
 }
+
+// XXH3-128 of an arbitrary key.
+LSMB_HD H128 xxh3_128(const uint8_t* p, uint64_t len) { return xxh3_128_r(xx::PtrReader{p}, len); }
 
 // Fixed 16-byte key given as its two LE u64 halves.
 LSMB_HD H128 xxh3_16(uint64_t lo, uint64_t hi) { return xx::len9to16(lo, hi, 16); }
