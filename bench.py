@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory end-to-end measurement")
     ap.add_argument("--no-varlen", action="store_true", help="skip the C4 variable-length build leg")
     ap.add_argument("--varlen-keys", type=int, default=100_000_000)
+    ap.add_argument("--filter-keys", type=int, default=0, help="size the filter for this many keys (default: all ranks' keys)")
     return ap.parse_args()
 
 
@@ -101,7 +102,10 @@ def main():
 
     npg = args.keys_per_gpu
     total = npg * world
-    nb, k = lsmbloom.params(total, 0.01)
+    # --filter-keys: size the filter for a larger global run than this job's
+    # keys (rehearses the per-GPU build of an N-GPU run on one GPU; C5's
+    # 1e9-key filter saturates at 2^32-1 bits).  Reported in config.
+    nb, k = lsmbloom.params(args.filter_keys or total, 0.01)
     nw = lsmbloom.num_words(nb)
     keys = torch.empty((npg, 16), dtype=torch.uint8, device=dev)
     ctx.gen_key16_dev(SEED_MEMBERS, rank * npg, npg, keys)
@@ -163,6 +167,8 @@ def main():
                                   % (total, npg),
                       "keys_per_gpu": npg, "global_keys": total, "num_bits": nb, "k": k,
                       "filter_bytes": 8 * nw, "strategy": strategy, "parallelism": "dp%d" % world}}
+    if args.filter_keys:
+        out["config"]["filter_sized_for_keys"] = args.filter_keys
     out["roofline"] = roof
 
     if args.verify and rank == 0 and world == 1:

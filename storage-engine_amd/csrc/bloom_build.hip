@@ -230,8 +230,15 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
 #pragma unroll
         for (int q = 0; q < KMAX; q++) {
             if (EXACT || (uint32_t)q < k) {
-                const uint32_t inc = FULL ? kinc : (pos[q] < sink ? kInc : 0u);
-                got[q] = (LSMB_ABL & 2) ? pos[q] : atomicAdd(fill + (pos[q] >> kSliceLog2), inc);
+                if (FULL) {
+                    got[q] = (LSMB_ABL & 2) ? pos[q] : atomicAdd(fill + (pos[q] >> kSliceLog2), kinc);
+                } else {
+                    // A sweep keeps ~nb/nbins of the positions: the others are
+                    // masked off rather than sent to the sink, whose single
+                    // fill word and slot would serialise them (same-address
+                    // LDS atomics and writes).
+                    got[q] = pos[q] < sink ? atomicAdd(fill + (pos[q] >> kSliceLog2), kInc) : 0u;
+                }
             }
         }
         // Next phase's key: hash while the claims are in flight.
@@ -249,7 +256,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
                 const uint32_t tgt = got[q] < lim ? b * R4 + x : nb * R4;
                 if (LSMB_ABL & 2)
                     gmax ^= tgt;
-                else
+                else if (FULL || pos[q] < sink)
                     *(uint32_t*)((char*)sm + tgt) = pos[q] & kSliceMask;
                 if (!(LSMB_ABL & 2)) gmax = max(gmax, got[q]);
             }

@@ -38,8 +38,8 @@ struct LdsReader {
 // 0-16 / 17-128 / 129-240 / long paths otherwise (tools/mb_varhash.hip).
 // Keys that do not fit the window start another round at the first unhashed
 // key; a key longer than the whole window is hashed from global memory.
-constexpr uint32_t kHashWin = 40 * 1024;
-constexpr uint32_t kHashPieces = kHashWin / (256 * 16);  // 16-B loads per thread per round
+constexpr uint32_t kHashKeys = 256;       // keys (= threads) per workgroup
+constexpr uint32_t kHashWin = 40 * 1024;  // LDS window bytes
 
 __device__ __forceinline__ uint32_t len_class(uint64_t len) {
     if (len <= 16) return 0;
@@ -47,16 +47,18 @@ __device__ __forceinline__ uint32_t len_class(uint64_t len) {
     return 9;
 }
 
-template <int MODE = 0>
-__global__ __launch_bounds__(256) void k_hash_var(const uint8_t* __restrict__ d, const uint64_t* __restrict__ o,
-                                                  uint64_t n, uint4* __restrict__ out) {
-    __shared__ uint32_t win[kHashWin / 4 + 8];
-    __shared__ uint64_t ks_a[256], ks_b[256];
+template <int MODE = 0, uint32_t KEYS = kHashKeys, uint32_t WIN = kHashWin>
+__global__ __launch_bounds__(KEYS) void k_hash_var(const uint8_t* __restrict__ d, const uint64_t* __restrict__ o,
+                                                   uint64_t n, uint4* __restrict__ out) {
+    constexpr uint32_t kPieces = WIN / (KEYS * 16);  // 16-B loads per thread per round
+    static_assert(kPieces * KEYS * 16 == WIN, "window must be a whole number of rounds of loads");
+    __shared__ uint32_t win[WIN / 4 + 8];
+    __shared__ uint64_t ks_a[KEYS], ks_b[KEYS];
     __shared__ uint32_t cls_cnt[16];
-    __shared__ uint16_t perm[256];
+    __shared__ uint16_t perm[KEYS];
     const uint32_t t = threadIdx.x;
-    const uint64_t i0 = (uint64_t)blockIdx.x * 256;
-    const uint32_t m = (uint32_t)min<uint64_t>(256, n - i0);
+    const uint64_t i0 = (uint64_t)blockIdx.x * KEYS;
+    const uint32_t m = (uint32_t)min<uint64_t>(KEYS, n - i0);
     // key offsets to LDS; lane assignment by length class
     uint64_t a0 = 0, b0 = 0;
     if (t < m) {
@@ -85,17 +87,17 @@ __global__ __launch_bounds__(256) void k_hash_var(const uint8_t* __restrict__ d,
         // Every 16-B piece loaded holds at least one key byte, so no load
         // leaves the data's pages.
         const uintptr_t A = (uintptr_t)(d + ks_a[f]) & ~(uintptr_t)15;
-        const uintptr_t wend = min(A + (uintptr_t)kHashWin, end);
+        const uintptr_t wend = min(A + (uintptr_t)WIN, end);
         const uint32_t nb = (uint32_t)(wend - A);
-        uint4 v[kHashPieces];
+        uint4 v[kPieces];
 #pragma unroll
-        for (uint32_t r = 0; r < kHashPieces; r++) {
-            const uint32_t q = (r * 256 + t) * 16;
+        for (uint32_t r = 0; r < kPieces; r++) {
+            const uint32_t q = (r * KEYS + t) * 16;
             v[r] = q < nb ? ld_stream16((const uint4*)(A + q)) : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
-        for (uint32_t r = 0; r < kHashPieces; r++) {
-            const uint32_t q = (r * 256 + t) * 16;
+        for (uint32_t r = 0; r < kPieces; r++) {
+            const uint32_t q = (r * KEYS + t) * 16;
             if (q < nb) *(uint4*)((char*)win + q) = v[r];
         }
         __syncthreads();

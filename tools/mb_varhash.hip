@@ -77,10 +77,17 @@ int main(int argc, char** argv) {
         const float t_stage = timeit([&] { k_hash_var<1><<<g, 256>>>(d, o, n, out); });
         const float t_lds = timeit([&] { k_hash_var<0><<<g, 256>>>(d, o, n, out); });
         const float t_dir = timeit([&] { k_hash_direct<<<g, 256>>>(d, o, n, out); });
+        const uint32_t g2 = (uint32_t)((n + 127) / 128);
+        const float t_128_20 = timeit([&] { k_hash_var<0, 128, 20480><<<g2, 128>>>(d, o, n, out); });
+        const float t_128_24 = timeit([&] { k_hash_var<0, 128, 24576><<<g2, 128>>>(d, o, n, out); });
+        const float t_256_32 = timeit([&] { k_hash_var<0, 256, 32768><<<g, 256>>>(d, o, n, out); });
+        const uint32_t g3 = (uint32_t)((n + 63) / 64);
+        const float t_64_12 = timeit([&] { k_hash_var<0, 64, 12288><<<g3, 64>>>(d, o, n, out); });
         CK(hipDeviceSynchronize());
-        printf("mode %d (%s): %.1f B/key  stage-only %.3f ms (%.0f GB/s)  lds-hash %.3f ms  direct-hash %.3f ms\n", mode,
+        printf("mode %d (%s): %.1f B/key  stage-only %.3f ms (%.0f GB/s)  lds-hash %.3f ms  direct-hash %.3f ms"
+               "  | 128/20K %.3f  128/24K %.3f  256/32K %.3f  64/12K %.3f\n", mode,
                mode == 0 ? "8-256" : mode == 1 ? "132" : mode == 2 ? "64" : "200", (double)bytes / n, t_stage,
-               (bytes + 24.0 * n) / t_stage / 1e6, t_lds, t_dir);
+               (bytes + 24.0 * n) / t_stage / 1e6, t_lds, t_dir, t_128_20, t_128_24, t_256_32, t_64_12);
         fflush(stdout);
         CK(hipFree(d));
         CK(hipFree(o));
