@@ -39,8 +39,10 @@ __device__ __forceinline__ void store_row(uint8_t* out, uint64_t i, uint32_t str
 }
 
 // T holds up to 8*sizeof(T) filters' bits per position.
-template <class Src, typename T>
-__global__ __launch_bounds__(256) void k_probe_sliced(Src src, uint64_t n, Mod32 md, uint32_t k,
+// W: Walk32 when num_bits <= 2^31 (every intermediate fits 32 bits), else
+// Walk64.  K > 0: k fixed at compile time (7 = BloomFilter::new at fpr 0.01).
+template <class Src, typename T, class W, int K>
+__global__ __launch_bounds__(256) void k_probe_sliced(Src src, uint64_t n, Mod32 md, uint32_t k_,
                                                       uint32_t num_bits,
                                                       const ProbeFilter* __restrict__ filters,
                                                       uint32_t nfilt, uint32_t stride,
@@ -48,15 +50,30 @@ __global__ __launch_bounds__(256) void k_probe_sliced(Src src, uint64_t n, Mod32
     extern __shared__ __align__(16) uint8_t smem_raw[];
     T* table = reinterpret_cast<T*>(smem_raw);
     const uint32_t nw32 = (num_bits + 31) / 32;
+    // The filters' word pointers and output bits, loaded once and all at
+    // once (a per-filter descriptor -> word load chain would serialise 2F
+    // global round trips before the first key).
+    constexpr uint32_t FMAX = 8 * sizeof(T);
+    const uint32_t* wp[FMAX];
+    uint32_t ob[FMAX];
+#pragma unroll
+    for (uint32_t f = 0; f < FMAX; f++) {
+        wp[f] = f < nfilt ? filters[f].words32 : nullptr;
+        ob[f] = f < nfilt ? filters[f].out_bit : 0;
+    }
     for (uint32_t w = threadIdx.x; w < nw32; w += blockDim.x) {
+        uint32_t xs[FMAX];
+#pragma unroll
+        for (uint32_t f = 0; f < FMAX; f++) xs[f] = f < nfilt ? wp[f][w] : 0u;
         T acc[32];
 #pragma unroll
         for (int b = 0; b < 32; b++) acc[b] = 0;
-        for (uint32_t f = 0; f < nfilt; f++) {
-            const uint32_t x = filters[f].words32[w];
-            const uint32_t ob = filters[f].out_bit;
 #pragma unroll
-            for (int b = 0; b < 32; b++) acc[b] |= (T)((T)((x >> b) & 1u) << ob);
+        for (uint32_t f = 0; f < FMAX; f++) {
+            if (f < nfilt) {
+#pragma unroll
+                for (int b = 0; b < 32; b++) acc[b] |= (T)((T)((xs[f] >> b) & 1u) << ob[f]);
+            }
         }
 #pragma unroll
         for (int b = 0; b < 32; b++) table[w * 32 + b] = acc[b];
@@ -65,13 +82,25 @@ __global__ __launch_bounds__(256) void k_probe_sliced(Src src, uint64_t n, Mod32
     T all = 0;
     for (uint32_t f = 0; f < nfilt; f++) all |= (T)((T)1 << filters[f].out_bit);
     const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
-        H128 h = src.hash(i);
-        PosWalk pw(md, h.lo, h.hi);
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    typename Src::Pre pre = src.fetch(i, i < n);  // next key's load is in flight while this one hashes
+    for (; i < n; i += gs) {
+        const typename Src::Pre cur = pre;
+        pre = src.fetch(i + gs, i + gs < n);
+        H128 h = src.hash_pre(cur, i);
+        W pw(md, h.lo, h.hi);
         T m = all;
-        for (uint32_t j = 0; j < k; j++) {
-            m &= table[pw.pos()];
-            pw.next(md);
+        if (K > 0) {
+#pragma unroll
+            for (int j = 0; j < K; j++) {
+                m &= table[pw.pos()];
+                if (j + 1 < K) pw.next(md);
+            }
+        } else {
+            for (uint32_t j = 0; j < k_; j++) {
+                m &= table[pw.pos()];
+                pw.next(md);
+            }
         }
         store_row<T>(out, i, stride, m);
     }
@@ -185,9 +214,18 @@ hipError_t probe_with(const Src& src, uint64_t n, const ProbeFilter* hf, uint32_
                 kern<<<dim3((uint32_t)g), dim3(256), smem, st>>>(src, n, hf[0].md, hf[0].k, nb, df, nfilt,
                                                                  stride, out);
             };
-            if (tsz == 1) go(k_probe_sliced<Src, uint8_t>);
-            else if (tsz == 2) go(k_probe_sliced<Src, uint16_t>);
-            else go(k_probe_sliced<Src, uint32_t>);
+            const bool w32 = fits_walk32(nb), k7 = hf[0].k == 7;
+            if (tsz == 1) {
+                if (w32 && k7) go(k_probe_sliced<Src, uint8_t, Walk32, 7>);
+                else if (w32) go(k_probe_sliced<Src, uint8_t, Walk32, 0>);
+                else go(k_probe_sliced<Src, uint8_t, Walk64, 0>);
+            } else if (tsz == 2) {
+                if (w32) go(k_probe_sliced<Src, uint16_t, Walk32, 0>);
+                else go(k_probe_sliced<Src, uint16_t, Walk64, 0>);
+            } else {
+                if (w32) go(k_probe_sliced<Src, uint32_t, Walk32, 0>);
+                else go(k_probe_sliced<Src, uint32_t, Walk64, 0>);
+            }
             return hipGetLastError();
         }
     }
