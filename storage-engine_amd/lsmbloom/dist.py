@@ -57,6 +57,9 @@ def or_allreduce_(words, group=None, ctx=None):
     n = words.numel()
     mine, _ = or_reduce_scatter_(words, group, ctx)
     per = mine.numel()
+    if per * world == n and words.is_contiguous():
+        dist.all_gather_into_tensor(words, mine, group=group)  # no staging copy (C5: 2^26 words)
+        return words
     out = torch.empty(per * world, dtype=words.dtype, device=words.device)
     dist.all_gather_into_tensor(out, mine, group=group)
     words.copy_(out[:n])

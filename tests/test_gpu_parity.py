@@ -116,6 +116,15 @@ def test_build_partition_huge_filter(ctx, oracle):
     _cmp(ctx.build_fixed(keys, 16, nb, k), oracle.build_fixed_mt(keys, 16, nb, k, 16))
 
 
+@pytest.mark.parametrize("n,filter_keys", [(24_000_000, 200_000_000), (20_000_000, 10**9)])
+def test_build_multi_sweep_steady_state(ctx, oracle, n, filter_keys):
+    # pass A sweeps (> 1024 slices): 2 sweeps at a 2-GPU run's filter, 4 at C5's
+    keys = keygen.key16(0x5EED0001, 0, n)
+    nb, k = lsmbloom.params(filter_keys, 0.01)
+    assert lsmbloom.build_strategy(nb, n) == "partition"
+    _cmp(ctx.build_fixed(keys, 16, nb, k), oracle.build_fixed_mt(keys, 16, nb, k, 16))
+
+
 def test_build_few_keys_huge_filter_atomic(ctx, oracle):
     nb, k = lsmbloom.params(10**8, 0.01)
     keys = keygen.key16(0x1234, 0, 1000)

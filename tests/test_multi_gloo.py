@@ -46,7 +46,8 @@ def _worker(rank, world, port, n, nbits, k, q):
 
 
 @pytest.mark.parametrize("world,n,nbits", [(2, 200_000, 1_917_011), (3, 150_001, 3_000_017),
-                                           (2, 50_000, 64 * 1001)])
+                                           (2, 50_000, 64 * 1001), (2, 50_000, 64 * 1000),
+                                           (4, 80_000, 64 * 4096)])
 def test_sharded_build_or_allreduce(oracle, world, n, nbits):
     import keygen
     k = 7
