@@ -160,8 +160,13 @@ __device__ __forceinline__ uint64_t pack3(uint32_t x, uint32_t y, uint32_t z) {
 // BloomFilter::new yields for fpr = 0.01).
 constexpr uint32_t kAhead = 4;  // pass A key prefetch distance, in phases
 
-template <class Src, class W, int KMAX, bool EXACT, bool FULL>
+// PER: keys per lane per phase.  Sweeps (!FULL) keep ~1/sweeps of the
+// positions, so their phases take two keys per lane: half the barriers and
+// flush rounds per key (PartitionPlan::keys_per_lane; the ring is sized for it).
+template <class Src, class W, int KMAX, bool EXACT, bool FULL, int PER = 1>
 __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md, uint32_t k_, PassA a) {
+    static_assert(PER == 1 || EXACT, "two keys per lane: exact k only");
+    constexpr int NP = PER * KMAX;  // positions per lane per phase
     extern __shared__ uint32_t sm[];
     const uint32_t k = EXACT ? (uint32_t)KMAX : k_;
     const uint32_t R = a.ring, R4 = 4 * a.ring, nb = a.nb;
@@ -181,7 +186,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
     // Workgroup w owns keys [w*per, (w+1)*per): a contiguous, coalesced run.
     const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
     const uint64_t i0 = (uint64_t)w * per, i1 = min(n, i0 + per);
-    const uint64_t iters = i1 > i0 ? (i1 - i0 + kBinBlock - 1) / kBinBlock : 0;  // uniform over the workgroup
+    const uint64_t iters = i1 > i0 ? (i1 - i0 + PER * kBinBlock - 1) / (PER * kBinBlock) : 0;  // uniform
     const uint32_t spw = (nb + 15) / 16;  // slices per wave (<= 64)
     const uint32_t own = wave * spw + lane;
     const bool owner = lane < spw && own < nb;
@@ -189,8 +194,8 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
 
     // Local positions (p - b0 * 2^20) of the key this lane claims in the
     // current phase; `sink` where there is none.  kinc: this key's increment.
-    uint32_t pos[KMAX], kinc = 0;
-    auto walk_positions = [&](const H128& h, bool ok, uint32_t (&out)[KMAX]) {
+    uint32_t pos[NP], kinc[PER];
+    auto walk_positions = [&](const H128& h, bool ok, uint32_t* out) {
         W walk(md, h.lo, h.hi);
 #pragma unroll
         for (int q = 0; q < KMAX; q++) {
@@ -201,37 +206,44 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
             }
         }
     };
-    auto key_index = [&](uint64_t it) { return i0 + it * kBinBlock + tid; };
-    auto key_ok = [&](uint64_t it) { return it < iters && key_index(it) < i1; };
+    // a lane's keys of phase `it`: key_index(it) + j, j < PER
+    auto key_index = [&](uint64_t it) { return i0 + (it * kBinBlock + tid) * PER; };
+    auto key_ok = [&](uint64_t it, int j = 0) { return it < iters && key_index(it) + j < i1; };
+    using Pre = typename Src::Pre;
+    auto fetch_keys = [&](uint64_t it, Pre (&out)[PER]) {
+#pragma unroll
+        for (int j = 0; j < PER; j++) out[j] = src.fetch(key_index(it) + j, key_ok(it, j));
+    };
     // Keys are loaded kAhead phases before they are hashed, into kAhead
     // buffers with static roles (the loop is unrolled kAhead times, so no
     // register copy forces a vmcnt drain).  gfx9 retires loads and stores in
     // one in-order vmcnt queue: a key load completes only after every older
     // region store, so the distance must cover the store round trip too.
-    typename Src::Pre pb0, pb1, pb2, pb3;  // key m lives in pb[m % 4]
-    {
-        const bool ok = key_ok(0);
-        const typename Src::Pre p = src.fetch(key_index(0), ok);
-        const H128 h = ok ? src.hash_pre(p, key_index(0)) : H128{0, 0};
-        walk_positions(h, ok, pos);
-        kinc = ok ? kInc : 0u;
+    Pre pb0[PER], pb1[PER], pb2[PER], pb3[PER];  // phase m's keys live in pb[m % 4]
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+        const bool ok = key_ok(0, j);
+        const Pre p = src.fetch(key_index(0) + j, ok);
+        const H128 h = ok ? src.hash_pre(p, key_index(0) + j) : H128{0, 0};
+        walk_positions(h, ok, pos + j * KMAX);
+        kinc[j] = ok ? kInc : 0u;
     }
-    pb1 = src.fetch(key_index(1), key_ok(1));
-    pb2 = src.fetch(key_index(2), key_ok(2));
-    pb3 = src.fetch(key_index(3), key_ok(3));
-    pb0 = src.fetch(key_index(4), key_ok(4));
+    fetch_keys(1, pb1);
+    fetch_keys(2, pb2);
+    fetch_keys(3, pb3);
+    fetch_keys(4, pb0);
     __syncthreads();
 
     // One phase: claim key it's positions, hash key it+1 (from `pre`) and
     // reload `pre` with key it+1+kAhead, store the entries, flush.
-    auto phase = [&](uint64_t it, typename Src::Pre& pre) __attribute__((always_inline)) {
-        // Claims for this phase's key, back to back.
-        uint32_t got[KMAX];
+    auto phase = [&](uint64_t it, Pre (&pre)[PER]) __attribute__((always_inline)) {
+        // Claims for this phase's keys, back to back.
+        uint32_t got[NP];
 #pragma unroll
-        for (int q = 0; q < KMAX; q++) {
+        for (int q = 0; q < NP; q++) {
             if (EXACT || (uint32_t)q < k) {
                 if (FULL) {
-                    got[q] = (LSMB_ABL & 2) ? pos[q] : atomicAdd(fill + (pos[q] >> kSliceLog2), kinc);
+                    got[q] = (LSMB_ABL & 2) ? pos[q] : atomicAdd(fill + (pos[q] >> kSliceLog2), kinc[q / KMAX]);
                 } else {
                     // A sweep keeps ~nb/nbins of the positions: the others are
                     // masked off rather than sent to the sink, whose single
@@ -241,14 +253,19 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
                 }
             }
         }
-        // Next phase's key: hash while the claims are in flight.
-        const bool nok = key_ok(it + 1);
-        const H128 nh = src.hash_pre(pre, key_index(it + 1));
-        pre = src.fetch(key_index(it + 1 + kAhead), key_ok(it + 1 + kAhead));
+        // Next phase's keys: hash while the claims are in flight.
+        bool nok[PER];
+        H128 nh[PER];
+#pragma unroll
+        for (int j = 0; j < PER; j++) {
+            nok[j] = key_ok(it + 1, j);
+            nh[j] = src.hash_pre(pre[j], key_index(it + 1) + j);
+        }
+        fetch_keys(it + 1 + kAhead, pre);
         // Store the claimed entries (overflowing claims into the sink's slot 0).
         uint32_t gmax = 0;
 #pragma unroll
-        for (int q = 0; q < KMAX; q++) {
+        for (int q = 0; q < NP; q++) {
             if (EXACT || (uint32_t)q < k) {
                 const uint32_t b = pos[q] >> kSliceLog2;
                 uint32_t x = got[q] & 0xFFFFu;
@@ -263,7 +280,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
         }
         if (__builtin_expect(__ballot(gmax >= lim) != 0, 0)) {
 #pragma unroll
-            for (int q = 0; q < KMAX; q++)
+            for (int q = 0; q < NP; q++)
                 if ((EXACT || (uint32_t)q < k) && got[q] >= lim && pos[q] < sink) {
                     or_pos_global(a.gw, a.b0 + (pos[q] >> kSliceLog2), pos[q] & kSliceMask);
 #ifdef LSMB_STATS
@@ -271,8 +288,11 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
 #endif
                 }
         }
-        walk_positions(nh, nok, pos);
-        kinc = nok ? kInc : 0u;
+#pragma unroll
+        for (int j = 0; j < PER; j++) {
+            walk_positions(nh[j], nok[j], pos + j * KMAX);
+            kinc[j] = nok[j] ? kInc : 0u;
+        }
         lds_barrier();
 
         // Flush: each owner lane writes its slice's full segment (usually
@@ -581,10 +601,17 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
             };
             const bool full = pl.sweeps == 1;
             if (k == 7) {
+                const bool two = pl.keys_per_lane == 2;
                 if (w32) {
-                    if (full) go(k_bin<Src, Walk32, 7, true, true>); else go(k_bin<Src, Walk32, 7, true, false>);
+                    if (full && two) go(k_bin<Src, Walk32, 7, true, true, 2>);
+                    else if (full) go(k_bin<Src, Walk32, 7, true, true>);
+                    else if (two) go(k_bin<Src, Walk32, 7, true, false, 2>);
+                    else go(k_bin<Src, Walk32, 7, true, false>);
                 } else {
-                    if (full) go(k_bin<Src, Walk64, 7, true, true>); else go(k_bin<Src, Walk64, 7, true, false>);
+                    if (full && two) go(k_bin<Src, Walk64, 7, true, true, 2>);
+                    else if (full) go(k_bin<Src, Walk64, 7, true, true>);
+                    else if (two) go(k_bin<Src, Walk64, 7, true, false, 2>);
+                    else go(k_bin<Src, Walk64, 7, true, false>);
                 }
             } else if (k <= 8) {
                 if (w32) go(k_bin<Src, Walk32, 8, false, false>); else go(k_bin<Src, Walk64, 8, false, false>);
@@ -654,6 +681,13 @@ PartitionPlan plan_partition(uint32_t num_bits, uint32_t k, uint64_t n, int num_
             pl.ring = r;
             break;
         }
+    }
+    // k = 7 builds take two keys per lane per phase when the ring still
+    // holds a phase's doubled arrivals (LSMB_SWEEP_PER=1 turns it off).
+    if (k == 7) {
+        const char* e = getenv("LSMB_SWEEP_PER");
+        const uint32_t need2 = (kSegEntries + (uint32_t)ceil(2 * lambda + 2.0 * sqrt(2 * lambda)) + 7) & ~7u;
+        if ((pl.ring >= need2 && !(e && atoi(e) == 1)) || (e && atoi(e) == 2)) pl.keys_per_lane = 2;
     }
     // one 1024-thread workgroup per CU, at least ~kBinBlock keys each
     const uint64_t gmax = (n + kBinBlock - 1) / kBinBlock;

@@ -48,6 +48,7 @@ struct PartitionPlan {
     uint32_t bins_per_sweep = 0;  // slices buffered in LDS per pass A launch
     uint32_t ring = 0;            // pass A ring entries per slice (multiple of 4, >= kSegEntries)
     uint32_t sweeps = 0;
+    uint32_t keys_per_lane = 1;   // pass A keys per lane per phase (2: k = 7 sweeps)
     uint64_t region_bytes = 0;    // nbins * grid * cap_segs * 64
     uint64_t counts_bytes = 0;    // nbins * grid * 4
 };
