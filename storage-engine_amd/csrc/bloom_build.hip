@@ -82,6 +82,41 @@ __global__ __launch_bounds__(1024) void k_build_lds(Src src, uint64_t n, Mod32 m
     }
 }
 
+// ---------------------------------------------------------------- Tiled strategy
+// Mid-size filters (160 KiB .. 4 MiB: compaction-sized SSTables).  Global
+// atomics on such a filter run at the memory side (device-scope atomics are
+// not L2-local across the 8 XCDs): ~26 G/s, 0.27 ms for 1 M keys.  Instead,
+// workgroup (c, s) zeroes one 2^20-bit slice in LDS, hashes key chunk c and
+// sets the positions that fall in slice s with ds_or, then stores the slice
+// to its scratch tile with plain coalesced stores.  Every key is hashed once
+// per slice (<= kTiledMaxSlices), which is cheaper than the atomics there.
+template <class Src>
+__global__ __launch_bounds__(1024) void k_build_tiled(Src src, uint64_t n, Mod32 md, uint32_t k, uint32_t nslices,
+                                                      uint32_t nw32, uint64_t stride32,
+                                                      uint32_t* __restrict__ tiles) {
+    extern __shared__ uint32_t sl[];
+    const uint32_t s = blockIdx.x % nslices, c = blockIdx.x / nslices, chunks = gridDim.x / nslices;
+    for (uint32_t w = threadIdx.x; w < kSliceWords32; w += 1024) sl[w] = 0;
+    __syncthreads();
+    const uint64_t per = (n + chunks - 1) / chunks;
+    const uint64_t i0 = (uint64_t)c * per, i1 = min(n, i0 + per);
+    for (uint64_t i = i0 + threadIdx.x; i < i1; i += 1024) {
+        const H128 h = src.hash(i);
+        Walk32 pw(md, h.lo, h.hi);
+        for (uint32_t j = 0; j < k; j++) {
+            const uint32_t p = pw.pos();
+            if ((p >> kSliceLog2) == s) atomicOr(&sl[(p & kSliceMask) >> 5], 1u << (p & 31));
+            pw.next(md);
+        }
+    }
+    __syncthreads();
+    const uint32_t w0 = s * kSliceWords32;
+    const uint32_t nw = min(kSliceWords32, nw32 - w0);
+    uint4* dst = reinterpret_cast<uint4*>(tiles + (uint64_t)c * stride32 + w0);
+    const uint4* srcw = reinterpret_cast<const uint4*>(sl);
+    for (uint32_t q = threadIdx.x; q < (nw + 3) / 4; q += 1024) dst[q] = srcw[q];
+}
+
 // ---------------------------------------------------------------- Atomic strategy
 template <class Src>
 __global__ __launch_bounds__(256) void k_build_atomic(Src src, uint64_t n, Mod32 md, uint32_t k,
@@ -563,6 +598,16 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
         set_max_lds((const void*)k_build_lds<Src>);
         k_build_lds<Src><<<dim3((uint32_t)g), dim3(1024), smem, st>>>(src, n, md, k, nw32, gw);
         if (tm) hipEventRecord(tm->t1, st);
+    } else if (s == BuildStrategy::Tiled) {
+        const TiledPlan tp = plan_tiled(num_bits, n, num_cus);
+        if (!ws.regions || tp.scratch_bytes > ws.region_bytes) return hipErrorInvalidValue;
+        uint32_t* tiles = reinterpret_cast<uint32_t*>(ws.regions);
+        set_max_lds((const void*)k_build_tiled<Src>);
+        k_build_tiled<Src><<<dim3(tp.chunks * tp.nslices), dim3(1024), kSliceWords32 * 4, st>>>(
+            src, n, md, k, tp.nslices, nw32, tp.stride32, tiles);
+        if (tm) hipEventRecord(tm->t1, st);
+        hipError_t e = launch_or_reduce(gw, tiles, nw32, tp.chunks, tp.stride32, st);
+        if (e != hipSuccess) return e;
     } else if (s == BuildStrategy::Atomic) {
         uint64_t g = (n + 255) / 256;
         if (g > (uint64_t)num_cus * 8) g = (uint64_t)num_cus * 8;
@@ -642,6 +687,7 @@ const char* strategy_name(BuildStrategy s) {
         case BuildStrategy::Lds: return "lds";
         case BuildStrategy::Partition: return "partition";
         case BuildStrategy::Atomic: return "atomic";
+        case BuildStrategy::Tiled: return "tiled";
     }
     return "?";
 }
@@ -655,6 +701,7 @@ BuildStrategy pick_build_strategy(uint32_t num_bits, uint32_t k, uint64_t n) {
     if (n * (uint64_t)k < nw32 / 16) return BuildStrategy::Atomic;
     // Fewer than 64 slices (< 8 MiB filters): too few LDS buffers to spread
     // a workgroup's claims; memory-side atomics on the small filter instead.
+    if (nw32 <= (uint64_t)kTiledMaxSlices * kSliceWords32 && k <= 32) return BuildStrategy::Tiled;
     if (nw32 < 64ull * kSliceWords32) return BuildStrategy::Atomic;
     return BuildStrategy::Partition;
 }
@@ -708,6 +755,21 @@ PartitionPlan plan_partition(uint32_t num_bits, uint32_t k, uint64_t n, int num_
     pl.region_bytes = fits ? (uint64_t)pl.nbins * pl.grid * pl.cap_segs * 64 : ~0ull >> 2;
     pl.counts_bytes = (uint64_t)pl.nbins * pl.grid * 4;
     return pl;
+}
+
+TiledPlan plan_tiled(uint32_t num_bits, uint64_t n, int num_cus) {
+    TiledPlan tp;
+    const uint64_t nw32 = 2 * (((uint64_t)num_bits + 63) / 64);
+    tp.nslices = (uint32_t)((nw32 + kSliceWords32 - 1) / kSliceWords32);
+    // ~2 workgroups per CU in all, at least 4 Ki keys per chunk
+    uint64_t ch = (2ull * (uint64_t)num_cus + tp.nslices - 1) / tp.nslices;
+    const uint64_t by_keys = (n + 4095) / 4096;
+    if (ch > by_keys) ch = by_keys;
+    if (ch < 1) ch = 1;
+    tp.chunks = (uint32_t)ch;
+    tp.stride32 = (uint64_t)tp.nslices * kSliceWords32;
+    tp.scratch_bytes = (uint64_t)tp.chunks * tp.stride32 * 4;
+    return tp;
 }
 
 uint64_t partition_chunk_keys(uint32_t num_bits, uint32_t k, uint64_t max_bytes, int num_cus) {

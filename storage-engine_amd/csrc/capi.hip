@@ -160,9 +160,18 @@ int build_dev(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k
     // LSMB_FORCE_STRATEGY=atomic: measurement override;
     // the filter is the same either way.
     if (const char* f = getenv("LSMB_FORCE_STRATEGY"))
-        if (s == BuildStrategy::Partition && !strcmp(f, "atomic")) s = BuildStrategy::Atomic;
+        if ((s == BuildStrategy::Partition || s == BuildStrategy::Tiled) && !strcmp(f, "atomic")) s = BuildStrategy::Atomic;
     c->tm.valid = false;
     if (s == BuildStrategy::None) return LSMB_OK;
+    if (s == BuildStrategy::Tiled) {
+        const TiledPlan tp = plan_tiled(num_bits, kb_all.n, c->num_cus);
+        HIP_TRY(c->ws_regions.ensure(tp.scratch_bytes));
+        PartitionWorkspace ws;
+        ws.regions = (uint64_t*)c->ws_regions.p;
+        ws.region_bytes = c->ws_regions.bytes;
+        HIP_TRY(launch_build(kb_all, num_bits, k, dw, s, ws, c->num_cus, st, c->timing ? &c->tm : nullptr));
+        return LSMB_OK;
+    }
     if (s != BuildStrategy::Partition) {
         HIP_TRY(launch_build(kb_all, num_bits, k, dw, s, PartitionWorkspace{}, c->num_cus, st, c->timing ? &c->tm : nullptr));
         return LSMB_OK;

@@ -32,7 +32,7 @@ struct KeyBatch {
     uint64_t n;
 };
 
-enum class BuildStrategy { None, Lds, Partition, Atomic };
+enum class BuildStrategy { None, Lds, Partition, Atomic, Tiled };
 
 BuildStrategy pick_build_strategy(uint32_t num_bits, uint32_t k, uint64_t n);
 const char* strategy_name(BuildStrategy s);
@@ -54,6 +54,17 @@ struct PartitionPlan {
 };
 
 PartitionPlan plan_partition(uint32_t num_bits, uint32_t k, uint64_t n, int num_cus);
+
+// Tiled strategy (filters of 2..kTiledMaxSlices slices): workgroup (c, s)
+// builds slice s from key chunk c in LDS and stores it to scratch tile
+// [c][s]; k_or_reduce then ORs the chunk tiles into the filter.
+constexpr uint32_t kTiledMaxSlices = 32;
+struct TiledPlan {
+    uint32_t nslices = 0, chunks = 0;
+    uint64_t stride32 = 0;       // u32 words per chunk tile row (nslices * 2^15)
+    uint64_t scratch_bytes = 0;  // chunks * stride32 * 4
+};
+TiledPlan plan_tiled(uint32_t num_bits, uint64_t n, int num_cus);
 
 // Largest key count whose plan fits `max_bytes` of workspace.
 uint64_t partition_chunk_keys(uint32_t num_bits, uint32_t k, uint64_t max_bytes, int num_cus);

@@ -125,6 +125,26 @@ def test_build_multi_sweep_steady_state(ctx, oracle, n, filter_keys):
     _cmp(ctx.build_fixed(keys, 16, nb, k), oracle.build_fixed_mt(keys, 16, nb, k, 16))
 
 
+@pytest.mark.parametrize("n,filter_keys", [(150_000, 150_000), (1_000_000, 1_000_000), (3_500_000, 3_500_000),
+                                           (50_000, 2_000_000)])
+def test_build_tiled_mid_size_filters(ctx, oracle, n, filter_keys):
+    # 160 KiB .. 4 MiB filters (compaction-sized SSTables): per-slice LDS tiles + OR-reduce
+    keys = keygen.key16(0x7117ED, 0, n)
+    nb, k = lsmbloom.params(filter_keys, 0.01)
+    assert lsmbloom.build_strategy(nb, n) == "tiled"
+    w = np.zeros(lsmbloom.num_words(nb), dtype=np.uint64)
+    w[::97] = 0x8000000000000001  # OR-accumulate into existing bits
+    ref = oracle.build_fixed(keys, 16, nb, k, words=w.copy())
+    _cmp(ctx.build_fixed(keys, 16, nb, k, words=w), ref)
+
+
+def test_build_tiled_varlen(ctx, oracle):
+    data, offs = keygen.varlen(400_000)
+    nb, k = lsmbloom.params(400_000, 0.01)
+    assert lsmbloom.build_strategy(nb, 400_000) == "tiled"
+    _cmp(ctx.build_var(data, offs, nb, k), oracle.build_var(data, offs, nb, k))
+
+
 def test_build_few_keys_huge_filter_atomic(ctx, oracle):
     nb, k = lsmbloom.params(10**8, 0.01)
     keys = keygen.key16(0x1234, 0, 1000)
