@@ -234,6 +234,29 @@ def bench_e2e(ctx, keys, n, nb, k, reps=3):
                      "pcie_GBs": round((n * 16 + size) / t / 1e9, 1)}
     res["value"] = res["pageable"]["value"]
     res["unit"] = "Mkeys/s"
+    # SST-sized flushes: one lsmb_build_block call per table, sized like
+    # SSTableBuilder::with_estimated_keys (builder.rs:74); latency per call
+    # (H2D, kernels, D2H, sync) next to the 1-thread CPU oracle on the same keys.
+    import oracle_ct
+    orc = oracle_ct.load()
+    small = []
+    for m in (1000, 100_000, 1_000_000):
+        nb_m, k_m = lsmbloom.params(m, 0.01)
+        ks = np.ascontiguousarray(host[: m * 16])
+        blk = np.empty(lsmbloom.serialized_size(nb_m), dtype=np.uint8)
+        ctx.build_block(ks, nb_m, k_m, key_len=16, out=blk)
+        ts = []
+        for _ in range(20):
+            t0 = time.perf_counter()
+            ctx.build_block(ks, nb_m, k_m, key_len=16, out=blk)
+            ts.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        ref = orc.build_fixed(ks.reshape(m, 16), 16, nb_m, k_m)
+        tc = time.perf_counter() - t0
+        small.append({"keys": m, "strategy": lsmbloom.build_strategy(nb_m, m),
+                      "gpu_ms": round(float(np.median(ts)) * 1e3, 3), "cpu_oracle_1t_ms": round(tc * 1e3, 3),
+                      "bit_exact": bool(np.array_equal(np.frombuffer(blk[12:].tobytes(), dtype=np.uint64), ref))})
+    res["sst_flush_latency"] = small
     return res
 
 

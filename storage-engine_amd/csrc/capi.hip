@@ -110,6 +110,9 @@ struct lsmb_ctx {
     DevBuf kslot[2], oslot[2];
     uint64_t* offs_pin[2] = {nullptr, nullptr};  // pinned rebased offsets per slot
     uint64_t offs_pin_cap[2] = {0, 0};
+    uint8_t* pin_small = nullptr;  // pinned staging of small host builds (host_build_small)
+    uint64_t pin_small_cap = 0;
+    bool ran_partition = false;    // a partition build ran since the last error-flag check
 };
 
 namespace {
@@ -142,6 +145,10 @@ int check_device_error(lsmb_ctx* c) {
         HIP_TRY(hipMemset((char*)c->err.p + 4, 0, 60));
     }
 #endif
+    // Only the partition kernels set the flag: skip the readback (a sync
+    // round trip) after builds that ran none.
+    if (!c->ran_partition) return LSMB_OK;
+    c->ran_partition = false;
     HIP_TRY(hipMemcpy(c->err_host, c->err.p, 32, hipMemcpyDeviceToHost));
     if (*c->err_host) {
         uint32_t e[8];
@@ -176,6 +183,7 @@ int build_dev(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k
         HIP_TRY(launch_build(kb_all, num_bits, k, dw, s, PartitionWorkspace{}, c->num_cus, st, c->timing ? &c->tm : nullptr));
         return LSMB_OK;
     }
+    c->ran_partition = true;
     uint64_t chunk = partition_chunk_keys(num_bits, k, workspace_limit_bytes(), c->num_cus);
     if (chunk == 0) return fail(LSMB_ENOMEM, "partition workspace limit too small");
     chunk = std::min(chunk, kb_all.n);
@@ -249,9 +257,66 @@ uint64_t h2d_chunk_bytes() {
 // (BloomFilter::new), else from those words (OR-accumulate); the finished words
 // are copied to words_out (host, any alignment: lsmb_build_block points it at
 // the serialized block body).  Synchronous.
+// Small host builds (an SST flush of a few thousand keys): one pinned staging
+// buffer, plain memcpys into and out of it and true async DMA on the build
+// stream — pageable copies would each stage synchronously — and no copy
+// stream.  Latency, not bandwidth, is what these calls pay.
+constexpr uint64_t kSmallHostBuild = 1ull << 20;  // bytes of keys + offsets + words
+
+int host_build_small(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
+                     uint32_t num_bits, uint32_t k, const uint64_t* words_in, uint8_t* words_out) {
+    const uint64_t nw = nwords64(num_bits);
+    const uint64_t base = offsets ? offsets[0] : 0;
+    const uint64_t kbytes = offsets ? offsets[n] - base : n * (uint64_t)key_len;
+    const uint64_t obytes = offsets ? (n + 1) * 8 : 0;
+    const uint64_t kpad = (kbytes + 15) & ~15ull, opad = (obytes + 15) & ~15ull;
+    const uint64_t need = kpad + opad + nw * 8 + 64;
+    if (c->pin_small_cap < need) {
+        if (c->pin_small) HIP_TRY(hipHostFree(c->pin_small));
+        c->pin_small = nullptr;
+        c->pin_small_cap = 0;
+        const uint64_t cap = std::max<uint64_t>(need, kSmallHostBuild + 64);
+        if (hipHostMalloc((void**)&c->pin_small, cap, 0) != hipSuccess)
+            return fail(LSMB_ENOMEM, "pinned staging (%llu B)", (unsigned long long)cap);
+        c->pin_small_cap = cap;
+    }
+    uint8_t* pk = c->pin_small;
+    uint64_t* po = (uint64_t*)(c->pin_small + kpad);
+    uint64_t* pw = (uint64_t*)(c->pin_small + kpad + opad);
+    HIP_TRY(c->words.ensure(nw * 8));
+    HIP_TRY(c->kslot[0].ensure(kpad + 16));
+    uint32_t* dw = (uint32_t*)c->words.p;
+    // the previous small build's D2H out of this buffer has completed (synchronous calls)
+    if (kbytes) memcpy(pk, data + base, kbytes);
+    if (kbytes) HIP_TRY(hipMemcpyAsync(c->kslot[0].p, pk, kbytes, hipMemcpyHostToDevice, c->st));
+    if (offsets) {
+        for (uint64_t j = 0; j <= n; j++) po[j] = offsets[j] - base;
+        HIP_TRY(c->oslot[0].ensure(obytes));
+        HIP_TRY(hipMemcpyAsync(c->oslot[0].p, po, obytes, hipMemcpyHostToDevice, c->st));
+    }
+    if (words_in) {
+        memcpy(pw, words_in, nw * 8);
+        HIP_TRY(hipMemcpyAsync(dw, pw, nw * 8, hipMemcpyHostToDevice, c->st));
+    } else {
+        HIP_TRY(hipMemsetAsync(dw, 0, nw * 8, c->st));
+    }
+    KeyBatch kb{(const uint8_t*)c->kslot[0].p, offsets ? (const uint64_t*)c->oslot[0].p : nullptr, key_len,
+                (!offsets && key_len == 0) ? 1 : n};
+    if (int rc = build_dev(c, kb, num_bits, k, dw, c->st)) return rc;
+    HIP_TRY(hipMemcpyAsync(pw, dw, nw * 8, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    memcpy(words_out, pw, nw * 8);
+    return check_device_error(c);
+}
+
 int host_build(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
                uint32_t num_bits, uint32_t k, const uint64_t* words_in, uint8_t* words_out) {
     const uint64_t nw = nwords64(num_bits);
+    {
+        const uint64_t kb = offsets ? offsets[n] - offsets[0] : n * (uint64_t)key_len;
+        if (kb + (offsets ? (n + 1) * 8 : 0) + nw * 8 <= kSmallHostBuild)
+            return host_build_small(c, data, offsets, key_len, n, num_bits, k, words_in, words_out);
+    }
     HIP_TRY(c->words.ensure(nw * 8));
     uint32_t* dw = (uint32_t*)c->words.p;
     if (words_in)
@@ -472,6 +537,7 @@ void lsmb_close(lsmb_ctx* c) {
             if (c->ev_built[s]) hipEventDestroy(c->ev_built[s]);
         }
         if (c->cst) hipStreamDestroy(c->cst);
+        if (c->pin_small) hipHostFree(c->pin_small);
         hipEventDestroy(c->tm.t0);
         hipEventDestroy(c->tm.t1);
         hipEventDestroy(c->tm.t2);
