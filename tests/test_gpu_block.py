@@ -137,3 +137,32 @@ def test_gen_varlen_dev_matches_keygen_and_builds_like_oracle(ctx, oracle):
     torch.cuda.synchronize()
     hd, ho = keygen.varlen(n)
     assert np.array_equal(w.cpu().numpy().view(np.uint64), oracle.build_var(hd, ho, nb, k))
+
+
+def test_hash_var_windows_giant_keys_unaligned(ctx, oracle):
+    """k_hash_var edge cases on the partition path: keys longer than the 40 KiB
+    LDS window (hashed from global memory), workgroups that need several window
+    rounds, runs of empty keys, and a data pointer that is not 16-B aligned."""
+    import torch
+    rng = np.random.default_rng(7)
+    lens = rng.integers(8, 257, size=300_000)
+    lens[1000:1400] = 0                         # empty keys
+    lens[5000] = 50_000                         # > window: global path
+    lens[5001] = 70_001
+    lens[9000:9256] = 3000                      # 768 KB in one workgroup: many rounds
+    lens[-1] = 41_000
+    offs = np.zeros(lens.size + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens)
+    data = keygen.stream_bytes(0xABCDEF, int(offs[-1]))
+    n = lens.size
+    nb, k = lsmbloom.params(20_000_000, 0.01)
+    assert lsmbloom.build_strategy(nb, n) == "partition"
+    ref = oracle.build_var(data, offs, nb, k)
+    dev = torch.device("cuda:0")
+    raw = torch.zeros(data.size + 64, dtype=torch.uint8, device=dev)
+    raw[5:5 + data.size] = torch.from_numpy(data).to(dev)
+    d_offs = torch.from_numpy(offs.view(np.int64).copy()).to(dev)
+    w = torch.zeros(lsmbloom.num_words(nb), dtype=torch.int64, device=dev)
+    ctx.build_var_dev(raw[5:], d_offs, n, nb, k, w)
+    torch.cuda.synchronize()
+    assert np.array_equal(w.cpu().numpy().view(np.uint64), ref)
