@@ -602,9 +602,24 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
         const TiledPlan tp = plan_tiled(num_bits, n, num_cus);
         if (!ws.regions || tp.scratch_bytes > ws.region_bytes) return hipErrorInvalidValue;
         uint32_t* tiles = reinterpret_cast<uint32_t*>(ws.regions);
-        set_max_lds((const void*)k_build_tiled<Src>);
-        k_build_tiled<Src><<<dim3(tp.chunks * tp.nslices), dim3(1024), kSliceWords32 * 4, st>>>(
-            src, n, md, k, tp.nslices, nw32, tp.stride32, tiles);
+        if (ws.hashes && ws.hash_bytes >= n * 16 && !std::is_same<Src, Hashed>::value) {
+            // every slice's workgroups re-read the keys: hash them once into
+            // 16-B records (L2/MALL-resident at these sizes) and tile over those
+            const uint64_t g = (n + 255) / 256;
+            if (g > 0x7FFFFFFFull) return hipErrorInvalidValue;
+            if constexpr (std::is_same<Src, VarLen>::value)
+                k_hash_var<0><<<dim3((uint32_t)g), dim3(256), 0, st>>>(src.d, src.o, n, ws.hashes);
+            else
+                k_hash<Src><<<dim3((uint32_t)g), dim3(256), 0, st>>>(src, n, ws.hashes);
+            const Hashed hs{ws.hashes};
+            set_max_lds((const void*)k_build_tiled<Hashed>);
+            k_build_tiled<Hashed><<<dim3(tp.chunks * tp.nslices), dim3(1024), kSliceWords32 * 4, st>>>(
+                hs, n, md, k, tp.nslices, nw32, tp.stride32, tiles);
+        } else {
+            set_max_lds((const void*)k_build_tiled<Src>);
+            k_build_tiled<Src><<<dim3(tp.chunks * tp.nslices), dim3(1024), kSliceWords32 * 4, st>>>(
+                src, n, md, k, tp.nslices, nw32, tp.stride32, tiles);
+        }
         if (tm) hipEventRecord(tm->t1, st);
         hipError_t e = launch_or_reduce(gw, tiles, nw32, tp.chunks, tp.stride32, st);
         if (e != hipSuccess) return e;

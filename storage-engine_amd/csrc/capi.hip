@@ -176,6 +176,11 @@ int build_dev(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k
         PartitionWorkspace ws;
         ws.regions = (uint64_t*)c->ws_regions.p;
         ws.region_bytes = c->ws_regions.bytes;
+        if (!getenv("LSMB_TILED_NO_PREHASH")) {  // measurement switch
+            HIP_TRY(c->ws_hashes.ensure(kb_all.n * 16));
+            ws.hashes = (uint4*)c->ws_hashes.p;
+            ws.hash_bytes = c->ws_hashes.bytes;
+        }
         HIP_TRY(launch_build(kb_all, num_bits, k, dw, s, ws, c->num_cus, st, c->timing ? &c->tm : nullptr));
         return LSMB_OK;
     }

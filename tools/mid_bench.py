@@ -9,9 +9,11 @@ for n in (150_000, 1_000_000, 3_500_000):
     ctx.gen_key16_dev(0x5EED0001, 0, n, keys)
     w = torch.zeros(lsmbloom.num_words(nb), dtype=torch.int64, device=dev)
     res = {}
-    for mode in ("default", "atomic"):
+    for mode in ("default", "no_prehash", "atomic"):
+        os.environ.pop("LSMB_FORCE_STRATEGY", None)
+        os.environ.pop("LSMB_TILED_NO_PREHASH", None)
         if mode == "atomic": os.environ["LSMB_FORCE_STRATEGY"] = "atomic"
-        else: os.environ.pop("LSMB_FORCE_STRATEGY", None)
+        if mode == "no_prehash": os.environ["LSMB_TILED_NO_PREHASH"] = "1"
         ts = []
         for r in range(12):
             w.zero_(); ctx.build_fixed_dev(keys, 16, n, nb, k, w); ctx.sync(); torch.cuda.synchronize()
