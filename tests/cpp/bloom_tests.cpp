@@ -202,6 +202,18 @@ int main(int argc, char** argv) {
             CHECK(bf.words() == ref.words());
             CHECK(bf.serialize() == ref.serialize());
         });
+        run("build_serialized == build().serialize() (SSTableBuilder::finish, builder.rs:177-179)", [] {
+            BloomFilterBuilder b(1000, 0.01), b2(1000, 0.01);
+            char k[16];
+            for (int i = 0; i < 700; i++) {
+                snprintf(k, sizeof k, "blk_%06d", i);
+                b.add_key(k);
+                b2.add_key(k);
+            }
+            BloomFilterBuilder empty(1000, 0.01);
+            CHECK(b.build_serialized() == b2.build().serialize());
+            CHECK(empty.build_serialized() == BloomFilter(1000, 0.01).serialize());
+        });
         run("sstable bloom: existing found, absent rejected (integration_tests.rs:12-59)", [] {
             BloomFilterBuilder b(1000, 0.01);
             char k[16];
