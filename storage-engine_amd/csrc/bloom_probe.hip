@@ -49,7 +49,7 @@ __global__ __launch_bounds__(256) void k_probe_sliced(Src src, uint64_t n, Mod32
                                                       uint8_t* __restrict__ out) {
     extern __shared__ __align__(16) uint8_t smem_raw[];
     T* table = reinterpret_cast<T*>(smem_raw);
-    const uint32_t nw32 = (num_bits + 31) / 32;
+    const uint32_t nw32 = (uint32_t)(((uint64_t)num_bits + 31) / 32);  // 64-bit: num_bits may be 2^32-1
     // The filters' word pointers and output bits, loaded once and all at
     // once (a per-filter descriptor -> word load chain would serialise 2F
     // global round trips before the first key).
@@ -205,7 +205,7 @@ hipError_t probe_with(const Src& src, uint64_t n, const ProbeFilter* hf, uint32_
     if (g < 1) g = 1;
     if (same && nfilt <= 32) {
         const uint32_t nb = hf[0].num_bits;
-        const size_t ent = (size_t)((nb + 31) / 32) * 32;
+        const size_t ent = (size_t)(((uint64_t)nb + 31) / 32) * 32;  // 64-bit: nb + 31 wraps at 2^32-1
         const size_t tsz = nfilt <= 8 ? 1 : nfilt <= 16 ? 2 : 4;
         const size_t smem = ent * tsz;
         if (smem <= 64 * 1024) {

@@ -113,7 +113,17 @@ def test_build_partition_huge_filter(ctx, oracle):
     assert nb == 2**32 - 1
     keys = keygen.key16(0x5EED0001, 0, n)
     assert lsmbloom.build_strategy(nb, n) == "partition"
-    _cmp(ctx.build_fixed(keys, 16, nb, k), oracle.build_fixed_mt(keys, 16, nb, k, 16))
+    w = ctx.build_fixed(keys, 16, nb, k)
+    ref = oracle.build_fixed_mt(keys, 16, nb, k, 16)
+    _cmp(w, ref)
+    # probe against the 2^32-1-bit filter: the bit-sliced table sizing once
+    # wrapped at 32 bits here (nb + 31) and answered 0 for every key
+    q = np.concatenate([keys[:50_000], keygen.key16(0x5EED0002, 0, 50_000)])
+    for nf in (1, 3):
+        got = ctx.probe([(w, nb, k)] * nf, q, key_len=16)
+        exp = oracle.probe([(ref, nb, k)] * nf, q, key_len=16)
+        assert np.array_equal(got, exp)
+        assert (got[:50_000] == (1 << nf) - 1).all()
 
 
 @pytest.mark.parametrize("n,filter_keys", [(24_000_000, 200_000_000), (20_000_000, 10**9)])
@@ -328,3 +338,48 @@ def test_c2_full_size_bit_exact(ctx, oracle):
     host = oracle.key16(0x5EED0001, 0, n)
     ref = oracle.build_fixed_mt(host, 16, nb, k, 16)
     _cmp(got, ref)
+
+
+def test_c5_full_size_shards_or_equal_monolithic(ctx):
+    """C5 data path at full size on one GPU: 1e9 16-B keys, filter new(1e9, 0.01)
+    (2^32-1 bits, 512 MiB).  Eight shard builds (one per would-be rank) merged
+    with the native OR-reduce must equal the monolithic build of all 1e9 keys
+    (OR is associative, commutative and idempotent), every sampled member must
+    probe positive, and the fill ratio must match 1 - exp(-kN/m).  These are
+    size-independent properties; the word-exact oracle comparison for this
+    filter is test_build_multi_sweep_steady_state."""
+    import math
+
+    import torch
+    dev = torch.device("cuda:0")
+    N, G = 1_000_000_000, 8
+    nb, k = lsmbloom.params(N, 0.01)
+    assert nb == 2**32 - 1
+    nw = lsmbloom.num_words(nb)
+    keys = torch.empty((N, 16), dtype=torch.uint8, device=dev)
+    ctx.gen_key16_dev(0x5EED0001, 0, N, keys)
+    mono = torch.zeros(nw, dtype=torch.int64, device=dev)
+    ctx.build_fixed_dev(keys, 16, N, nb, k, mono)
+    parts = torch.zeros((G, nw), dtype=torch.int64, device=dev)
+    per = N // G
+    for g in range(G):
+        ctx.build_fixed_dev(keys[g * per:(g + 1) * per], 16, per, nb, k, parts[g])
+    merged = torch.zeros(nw, dtype=torch.int64, device=dev)
+    ctx.or_reduce_dev(merged, parts, nw, G, nw)
+    ctx.sync()
+    torch.cuda.synchronize()
+    assert torch.equal(merged, mono)
+    del parts, merged
+    host_words = mono.cpu().numpy().view(np.uint64)
+    ones = int(np.unpackbits(host_words.view(np.uint8)).sum())
+    assert abs(ones / nb - (1 - math.exp(-k * N / nb))) < 1e-3, ones / nb
+    sample = keys[::1_000_003][:1000].contiguous()
+    hs = sample.cpu().numpy()
+    f = BloomFilter(host_words, k, nb)
+    assert all(f.may_contain(bytes(hs[i])) for i in range(0, hs.shape[0], 50))  # host single-key path
+    out = torch.zeros(sample.shape[0], dtype=torch.uint8, device=dev)
+    ctx.probe_dev([(mono, nb, k)], sample, sample.shape[0], out, key_len=16)
+    torch.cuda.synchronize()
+    assert bool(out.bool().all()), int(out.sum().item())
+    del keys, mono
+    torch.cuda.empty_cache()
