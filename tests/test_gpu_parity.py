@@ -383,3 +383,46 @@ def test_c5_full_size_shards_or_equal_monolithic(ctx):
     assert bool(out.bool().all()), int(out.sum().item())
     del keys, mono
     torch.cuda.empty_cache()
+
+
+def test_c4_full_size_properties(ctx, oracle):
+    """C4 at full size: 1e8 var-len keys (8-256 B, ~13.2 GB) on the device.
+    The monolithic build equals the OR of four shard builds (each shard's
+    offsets rebased to its own data slice), sampled members probe positive
+    (and agree with the host single-key path), and the fill ratio is analytic.
+    The word-exact oracle comparison of this path at smaller n is in
+    tests/test_gpu_block.py."""
+    import math
+
+    import torch
+    N, G = 100_000_000, 4
+    data, offs = ctx.gen_varlen_dev(N)
+    nb, k = lsmbloom.params(N, 0.01)
+    nw = lsmbloom.num_words(nb)
+    dev = data.device
+    mono = torch.zeros(nw, dtype=torch.int64, device=dev)
+    ctx.build_var_dev(data, offs, N, nb, k, mono)
+    merged = torch.zeros(nw, dtype=torch.int64, device=dev)
+    per = N // G
+    for g in range(G):
+        o0, o1 = int(offs[g * per].item()), int(offs[(g + 1) * per].item())
+        so = (offs[g * per:(g + 1) * per + 1] - o0).contiguous()
+        part = torch.zeros(nw, dtype=torch.int64, device=dev)
+        ctx.build_var_dev(data[o0:o1], so, per, nb, k, part)
+        merged |= part
+        del part, so
+    ctx.sync()
+    torch.cuda.synchronize()
+    assert torch.equal(merged, mono)
+    del merged
+    host_words = mono.cpu().numpy().view(np.uint64)
+    ones = int(np.unpackbits(host_words.view(np.uint8)).sum())
+    assert abs(ones / nb - (1 - math.exp(-k * N / nb))) < 1e-3, ones / nb
+    idx = list(range(0, N, 997_331))[:100]
+    f = BloomFilter(host_words, k, nb)
+    oh = offs.cpu().numpy()
+    for i in idx:
+        key = bytes(data[int(oh[i]):int(oh[i + 1])].cpu().numpy())
+        assert f.may_contain(key)
+    del data, offs, mono
+    torch.cuda.empty_cache()
