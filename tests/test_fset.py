@@ -112,6 +112,27 @@ def test_fset_fixed_len_keys_and_device_probe(oracle):
 
 
 @pytest.mark.gpu
+def test_fset_saturated_and_mixed_size_filters(oracle):
+    # one 2^32-1-bit filter (new(1e9, .01)) next to SST-sized ones in one set
+    ctx = lsmbloom.Context(0)
+    fs = FilterSet(ctx)
+    tables = {}
+    for t, (n, sized) in enumerate([(200_000, 10**9), (5000, 5000), (1000, 1000)]):
+        keys = keygen.key16(0x5EED0300 + t, 0, n)
+        rows = sorted(bytes(r) for r in keys)
+        nb, k = lsmbloom.params(sized, 0.01)
+        w = oracle.build_fixed(keys, 16, nb, k)
+        s = fs.add_filter(BloomFilter(w, k, nb), rows[0], rows[-1])
+        tables[s] = (w, nb, k, rows[0], rows[-1])
+    q = np.concatenate([keygen.key16(0x5EED0300 + t, 0, 1000) for t in range(3)]
+                       + [keygen.key16(0x5EED0400, 0, 5000)])
+    got = fs.probe(q, key_len=16)
+    assert [int(x) for x in got] == expected_masks(oracle, tables, [bytes(r) for r in q])
+    fs.close()
+    ctx.close()
+
+
+@pytest.mark.gpu
 def test_fset_add_remove_reuse_and_limits(oracle):
     ctx = lsmbloom.Context(0)
     fs = FilterSet(ctx)
