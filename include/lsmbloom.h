@@ -223,7 +223,10 @@ int lsmb_fset_probe_dev(lsmb_fset* fs, const void* d_data, const void* d_offsets
 /* ---- introspection ------------------------------------------------------- */
 
 /* Name of the build strategy the dispatcher picks for (num_bits, n), e.g.
- * "lds", "partition", "atomic" (for tests and bench reporting). */
+ * "lds", "tiled", "partition", "atomic" (for tests and bench reporting).
+ * Measurement switches read at build time: LSMB_FORCE_STRATEGY=atomic,
+ * LSMB_SWEEP_PER=1/2 (pass A keys per lane), LSMB_TILED_NO_PREHASH=1,
+ * LSMB_H2D_CHUNK_MB, LSMB_WORKSPACE_MB.  The filter bits never depend on them. */
 const char* lsmb_build_strategy(uint32_t num_bits, uint64_t n);
 
 /* Timing of the last device build on this context, in milliseconds, per phase
