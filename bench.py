@@ -171,6 +171,29 @@ def main():
         out["config"]["filter_sized_for_keys"] = args.filter_keys
     out["roofline"] = roof
 
+    if world > 1:
+        # Multi-GPU self-check (outside the timed region): one more sharded
+        # step (build + OR-allreduce); rank 0 then rebuilds the whole global
+        # key set alone, 100 M keys at a time, and compares every word.  OR is
+        # associative and idempotent, so the merged filter must be identical.
+        step()
+        torch.cuda.synchronize(dev)
+        if rank == 0:
+            try:
+                ref = torch.zeros_like(words)
+                for first in range(0, total, npg):
+                    m = min(npg, total - first)
+                    ctx.gen_key16_dev(SEED_MEMBERS, first, m, keys[:m])
+                    ctx.build_fixed_dev(keys[:m], 16, m, nb, k, ref)
+                ctx.sync()
+                torch.cuda.synchronize(dev)
+                out["multi_gpu_merged_equals_single_gpu_build"] = bool(torch.equal(ref, words))
+                del ref
+                ctx.gen_key16_dev(SEED_MEMBERS, rank * npg, npg, keys)  # this rank's shard again
+            except Exception as e:  # report, never lose the bench line
+                out["multi_gpu_check_error"] = repr(e)[:200]
+        dist.barrier()
+
     if args.verify and rank == 0 and world == 1:
         import oracle_ct
         orc = oracle_ct.load()
