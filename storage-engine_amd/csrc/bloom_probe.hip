@@ -136,10 +136,16 @@ __global__ __launch_bounds__(256) void k_probe_generic(Src src, uint64_t n,
 }
 
 // Lexicographic byte-string order, as Rust's `[u8]` Ord (a proper prefix
-// sorts first): <0, 0, >0.
+// sorts first): <0, 0, >0.  Eight bytes per step as big-endian u64 (unaligned
+// dwordx2 loads), the tail byte by byte.
 __device__ __forceinline__ int key_cmp(const uint8_t* a, uint64_t la, const uint8_t* b, uint32_t lb) {
     const uint64_t m = la < lb ? la : lb;
-    for (uint64_t i = 0; i < m; i++)
+    uint64_t i = 0;
+    for (; i + 8 <= m; i += 8) {
+        const uint64_t x = __builtin_bswap64(xx::ld64(a + i)), y = __builtin_bswap64(xx::ld64(b + i));
+        if (x != y) return x < y ? -1 : 1;
+    }
+    for (; i < m; i++)
         if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
     return la < lb ? -1 : (la > lb ? 1 : 0);
 }
@@ -160,11 +166,32 @@ __global__ __launch_bounds__(256) void k_fset_probe(Src src, uint64_t n, const R
         const uint8_t* kp = src.bytes(i);
         const uint64_t kl = src.key_len(i);
         uint64_t m = 0;
+        // Positions of the last (num_bits, k <= 8) walked: the store's SST
+        // filters all share one sizing (builder.rs:51,74), so one walk serves
+        // every table in range.
+        uint32_t cpos[8];
+        uint32_t cnb = 0, ck = 0;
         for (uint32_t f = 0; f < nfilt; f++) {
             const RangedFilter& R = fl[f];
             if (key_cmp(kp, kl, R.lo, R.lo_len) < 0 || key_cmp(kp, kl, R.hi, R.hi_len) > 0) continue;
             bool hit = true;
-            if (R.f.k) {
+            if (R.f.k && R.f.k <= 8) {
+                if (R.f.num_bits != cnb || R.f.k != ck) {
+                    PosWalk pw(R.f.md, h.lo, h.hi);
+#pragma unroll
+                    for (uint32_t j = 0; j < 8; j++) {
+                        if (j < R.f.k) {
+                            cpos[j] = pw.pos();
+                            pw.next(R.f.md);
+                        }
+                    }
+                    cnb = R.f.num_bits;
+                    ck = R.f.k;
+                }
+#pragma unroll
+                for (uint32_t j = 0; j < 8; j++)
+                    if (j < ck) hit = hit && ((R.f.words32[cpos[j] >> 5] >> (cpos[j] & 31)) & 1u);
+            } else if (R.f.k) {
                 PosWalk pw(R.f.md, h.lo, h.hi);
                 for (uint32_t j = 0; j < R.f.k; j++) {
                     const uint32_t p = pw.pos();
