@@ -208,13 +208,91 @@ __global__ __launch_bounds__(256) void k_fset_probe(Src src, uint64_t n, const R
     }
 }
 
+// Filter-set probe when every filter of the set shares (num_bits, k) and the
+// bit-sliced table fits LDS (the store's SST filters: new(1000, 0.01), 9 568
+// bits, k = 7): entry p of the table holds the set's bit p, one bit per
+// descriptor.  A key pays the range checks, then k LDS reads ANDed over all
+// in-range filters at once (bits read from L2 per filter in k_fset_probe).
+template <class Src, typename T, int K>
+__global__ __launch_bounds__(256) void k_fset_sliced(Src src, uint64_t n, const RangedFilter* __restrict__ filters,
+                                                     uint32_t nfilt, uint32_t k_, uint64_t* __restrict__ out) {
+    extern __shared__ __align__(16) uint8_t smem_raw[];
+    __shared__ RangedFilter fl[64];
+    T* table = reinterpret_cast<T*>(smem_raw);
+    for (uint32_t f = threadIdx.x; f < nfilt; f += blockDim.x) fl[f] = filters[f];
+    __syncthreads();
+    const uint32_t num_bits = fl[0].f.num_bits;
+    const Mod32 md = fl[0].f.md;
+    const uint32_t nw32 = (num_bits + 31) / 32;  // num_bits <= 2^19 here: no wrap
+    for (uint32_t w = threadIdx.x; w < nw32; w += blockDim.x) {
+        T acc[32];
+#pragma unroll
+        for (int b = 0; b < 32; b++) acc[b] = 0;
+        for (uint32_t f = 0; f < nfilt; f++) {
+            const uint32_t x = fl[f].f.words32[w];
+#pragma unroll
+            for (int b = 0; b < 32; b++) acc[b] |= (T)((T)((x >> b) & 1u) << f);
+        }
+#pragma unroll
+        for (int b = 0; b < 32; b++) table[w * 32 + b] = acc[b];
+    }
+    __syncthreads();
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
+        const H128 h = src.hash(i);
+        const uint8_t* kp = src.bytes(i);
+        const uint64_t kl = src.key_len(i);
+        T m = 0;
+        for (uint32_t f = 0; f < nfilt; f++) {
+            const RangedFilter& R = fl[f];
+            if (key_cmp(kp, kl, R.lo, R.lo_len) >= 0 && key_cmp(kp, kl, R.hi, R.hi_len) <= 0) m |= (T)((T)1 << f);
+        }
+        if (m) {
+            Walk32 pw(md, h.lo, h.hi);
+            if (K > 0) {
+#pragma unroll
+                for (int j = 0; j < K; j++) {
+                    m &= table[pw.pos()];
+                    if (j + 1 < K) pw.next(md);
+                }
+            } else {
+                for (uint32_t j = 0; j < k_; j++) {
+                    m &= table[pw.pos()];
+                    pw.next(md);
+                }
+            }
+        }
+        uint64_t o = 0;
+        for (uint32_t f = 0; f < nfilt; f++)
+            if ((m >> f) & 1) o |= 1ull << fl[f].f.out_bit;
+        out[i] = o;
+    }
+}
+
 template <class Src>
-hipError_t fset_probe_with(const Src& src, uint64_t n, const RangedFilter* df, uint32_t nfilt, uint64_t* out,
-                           int num_cus, hipStream_t st) {
+hipError_t fset_probe_with(const Src& src, uint64_t n, const RangedFilter* df, uint32_t nfilt, uint32_t shared_nb,
+                           uint32_t shared_k, uint64_t* out, int num_cus, hipStream_t st) {
     uint64_t g = (n + 255) / 256;
     const uint64_t gmax = (uint64_t)num_cus * 8;
     if (g > gmax) g = gmax;
     if (g < 1) g = 1;
+    if (shared_nb > 0 && shared_k > 0) {
+        const size_t tsz = nfilt <= 8 ? 1 : nfilt <= 16 ? 2 : nfilt <= 32 ? 4 : 8;
+        const size_t smem = (size_t)(((uint64_t)shared_nb + 31) / 32) * 32 * tsz;
+        if (smem <= 64 * 1024) {
+            auto go = [&](auto kern) {
+                hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+                kern<<<dim3((uint32_t)g), dim3(256), smem, st>>>(src, n, df, nfilt, shared_k, out);
+            };
+            if (tsz == 1) {
+                if (shared_k == 7) go(k_fset_sliced<Src, uint8_t, 7>);
+                else go(k_fset_sliced<Src, uint8_t, 0>);
+            } else if (tsz == 2) go(k_fset_sliced<Src, uint16_t, 0>);
+            else if (tsz == 4) go(k_fset_sliced<Src, uint32_t, 0>);
+            else go(k_fset_sliced<Src, uint64_t, 0>);
+            return hipGetLastError();
+        }
+    }
     k_fset_probe<Src><<<dim3((uint32_t)g), dim3(256), 0, st>>>(src, n, df, nfilt, out);
     return hipGetLastError();
 }
@@ -262,14 +340,14 @@ hipError_t probe_with(const Src& src, uint64_t n, const ProbeFilter* hf, uint32_
 
 }  // namespace
 
-hipError_t launch_fset_probe(const KeyBatch& kb, const RangedFilter* df, uint32_t nfilt, uint64_t* out,
-                             int num_cus, hipStream_t st) {
+hipError_t launch_fset_probe(const KeyBatch& kb, const RangedFilter* df, uint32_t nfilt, uint32_t shared_nb,
+                             uint32_t shared_k, uint64_t* out, int num_cus, hipStream_t st) {
     if (kb.n == 0) return hipSuccess;
     if (nfilt > 64) return hipErrorInvalidValue;
-    if (kb.offsets) return fset_probe_with(VarLen{kb.data, kb.offsets}, kb.n, df, nfilt, out, num_cus, st);
+    if (kb.offsets) return fset_probe_with(VarLen{kb.data, kb.offsets}, kb.n, df, nfilt, shared_nb, shared_k, out, num_cus, st);
     if (kb.key_len == 16 && (reinterpret_cast<uintptr_t>(kb.data) & 15) == 0)
-        return fset_probe_with(Fixed16{reinterpret_cast<const uint4*>(kb.data)}, kb.n, df, nfilt, out, num_cus, st);
-    return fset_probe_with(FixedN{kb.data, kb.key_len}, kb.n, df, nfilt, out, num_cus, st);
+        return fset_probe_with(Fixed16{reinterpret_cast<const uint4*>(kb.data)}, kb.n, df, nfilt, shared_nb, shared_k, out, num_cus, st);
+    return fset_probe_with(FixedN{kb.data, kb.key_len}, kb.n, df, nfilt, shared_nb, shared_k, out, num_cus, st);
 }
 
 hipError_t launch_probe(const KeyBatch& kb, const ProbeFilter* hf, uint32_t nfilt,

@@ -804,6 +804,7 @@ struct lsmb_fset {
     DevBuf ranges;  // every live slot's lo and hi keys
     DevBuf desc;    // RangedFilter[ndesc]
     uint32_t ndesc = 0;
+    uint32_t shared_nb = 0, shared_k = 0;  // (num_bits, k) of every live slot, or 0 when they differ
     bool dirty = true;
 };
 
@@ -848,6 +849,10 @@ int fset_refresh(lsmb_fset* fs) {
     HIP_TRY(fs->desc.ensure(sizeof(RangedFilter) * 64));
     if (!d.empty()) HIP_TRY(hipMemcpy(fs->desc.p, d.data(), sizeof(RangedFilter) * d.size(), hipMemcpyHostToDevice));
     fs->ndesc = (uint32_t)d.size();
+    fs->shared_nb = d.empty() ? 0 : d[0].f.num_bits;
+    fs->shared_k = d.empty() ? 0 : d[0].f.k;
+    for (const auto& r : d)
+        if (r.f.num_bits != fs->shared_nb || r.f.k != fs->shared_k) fs->shared_nb = fs->shared_k = 0;
     fs->dirty = false;
     return LSMB_OK;
 }
@@ -940,7 +945,7 @@ int lsmb_fset_probe_dev(lsmb_fset* fs, const void* d_data, const void* d_offsets
         return LSMB_OK;
     }
     KeyBatch kb{(const uint8_t*)d_data, (const uint64_t*)d_offsets, key_len, n};
-    HIP_TRY(launch_fset_probe(kb, (const RangedFilter*)fs->desc.p, fs->ndesc, (uint64_t*)d_out, fs->c->num_cus, st));
+    HIP_TRY(launch_fset_probe(kb, (const RangedFilter*)fs->desc.p, fs->ndesc, fs->shared_nb, fs->shared_k, (uint64_t*)d_out, fs->c->num_cus, st));
     return LSMB_OK;
 }
 
@@ -960,7 +965,7 @@ int lsmb_fset_probe(lsmb_fset* fs, const uint8_t* data, const uint64_t* offsets,
         memset(out_mask, 0, n * 8);
         return LSMB_OK;
     }
-    HIP_TRY(launch_fset_probe(kb, (const RangedFilter*)fs->desc.p, fs->ndesc, (uint64_t*)c->out.p, c->num_cus, c->st));
+    HIP_TRY(launch_fset_probe(kb, (const RangedFilter*)fs->desc.p, fs->ndesc, fs->shared_nb, fs->shared_k, (uint64_t*)c->out.p, c->num_cus, c->st));
     HIP_TRY(hipMemcpyAsync(out_mask, c->out.p, n * 8, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(hipStreamSynchronize(c->st));
     return LSMB_OK;

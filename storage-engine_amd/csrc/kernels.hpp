@@ -111,9 +111,11 @@ struct RangedFilter {
 };
 
 // out[i] bit s = (lo_s <= key i <= hi_s) && may_contain(filter s, key i), for
-// the nfilt (<= 64) descriptors at d_filters (device memory).
-hipError_t launch_fset_probe(const KeyBatch& kb, const RangedFilter* d_filters, uint32_t nfilt, uint64_t* d_out,
-                             int num_cus, hipStream_t st);
+// the nfilt (<= 64) descriptors at d_filters (device memory).  shared_nb /
+// shared_k: the (num_bits, k) every descriptor has, or 0 when they differ
+// (selects the bit-sliced LDS table).
+hipError_t launch_fset_probe(const KeyBatch& kb, const RangedFilter* d_filters, uint32_t nfilt, uint32_t shared_nb,
+                             uint32_t shared_k, uint64_t* d_out, int num_cus, hipStream_t st);
 
 hipError_t launch_probe(const KeyBatch& kb, const ProbeFilter* h_filters, uint32_t nfilt,
                         ProbeFilter* d_filters_scratch, uint8_t* d_out, int num_cus,

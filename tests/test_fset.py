@@ -183,3 +183,29 @@ def test_fset_add_rejects_corrupt_blocks_like_deserialize(oracle):
     assert [int(x) for x in fs.probe_keys([b"a", b"b", b"bz", b"c", b"c\x00"])] == [0, 1 << s, 1 << s, 1 << s, 0]
     fs.close()
     ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ntab,fpr", [(5, 0.05), (20, 0.01), (33, 0.001)])
+def test_fset_same_sized_sliced_table_widths(oracle, ntab, fpr):
+    # every filter of the set shares (num_bits, k): the bit-sliced LDS table
+    # path, at 8/32/64-bit entries and k != 7
+    ctx = lsmbloom.Context(0)
+    fs = FilterSet(ctx)
+    nb, k = lsmbloom.params(800, fpr)
+    tables = {}
+    for t in range(ntab):
+        keys = keygen.key16(0x5EED0500 + t, 0, 800)
+        rows = sorted(bytes(r) for r in keys)
+        w = oracle.build_fixed(keys, 16, nb, k)
+        lo, hi = rows[t % 3 * 100], rows[-1 - t % 5 * 100]
+        s = fs.add_filter(BloomFilter(w, k, nb), lo, hi)
+        tables[s] = (w, nb, k, lo, hi)
+    fs.remove(1)
+    del tables[1]
+    q = np.concatenate([keygen.key16(0x5EED0500 + t, 0, 300) for t in range(ntab)]
+                       + [keygen.key16(0x5EED0600, 0, 3000)])
+    got = fs.probe(q, key_len=16)
+    assert [int(x) for x in got] == expected_masks(oracle, tables, [bytes(r) for r in q])
+    fs.close()
+    ctx.close()
