@@ -150,6 +150,48 @@ __device__ __forceinline__ int key_cmp(const uint8_t* a, uint64_t la, const uint
     return la < lb ? -1 : (la > lb ? 1 : 0);
 }
 
+// A byte string's first 16 bytes, zero-padded, as two big-endian words.  Two
+// strings whose padded prefixes differ order as the prefixes do (a difference
+// inside the padding means the shorter one is a proper prefix of the other);
+// equal prefixes order by length when both fit 16 bytes, else by key_cmp.
+struct Pfx16 {
+    uint64_t w0, w1;
+    uint32_t len;
+};
+
+__device__ __forceinline__ Pfx16 prefix16(const uint8_t* p, uint64_t len) {
+    Pfx16 r;
+    r.len = len > 0xffffffffull ? 0xffffffffu : (uint32_t)len;
+    if (len >= 16) {
+        r.w0 = __builtin_bswap64(xx::ld64(p));
+        r.w1 = __builtin_bswap64(xx::ld64(p + 8));
+    } else {
+        r.w0 = r.w1 = 0;
+        for (uint32_t i = 0; i < (uint32_t)len; i++) {
+            const uint64_t b = p[i];
+            if (i < 8) r.w0 |= b << (56 - 8 * i);
+            else r.w1 |= b << (56 - 8 * (i - 8));
+        }
+    }
+    return r;
+}
+
+__device__ __forceinline__ int cmp_pfx(const Pfx16& k, const uint8_t* kp, uint64_t kl, const Pfx16& b,
+                                       const uint8_t* bp, uint32_t bl) {
+    if (k.w0 != b.w0) return k.w0 < b.w0 ? -1 : 1;
+    if (k.w1 != b.w1) return k.w1 < b.w1 ? -1 : 1;
+    if (kl <= 16 && bl <= 16) return kl < bl ? -1 : (kl > bl ? 1 : 0);
+    return key_cmp(kp, kl, bp, bl);
+}
+
+// Per workgroup: every descriptor's lo/hi prefixes into LDS.
+__device__ __forceinline__ void stage_bounds(const RangedFilter* fl, uint32_t nfilt, Pfx16* blo, Pfx16* bhi) {
+    for (uint32_t f = threadIdx.x; f < nfilt; f += blockDim.x) {
+        blo[f] = prefix16(fl[f].lo, fl[f].lo_len);
+        bhi[f] = prefix16(fl[f].hi, fl[f].hi_len);
+    }
+}
+
 // Filter-set probe (multi-get pre-check): per key, for every SSTable of the
 // set, the two checks SSTable::get makes before touching the index
 // (src/sstable/reader.rs:192-199): key inside [min_key, max_key], then
@@ -158,13 +200,17 @@ template <class Src>
 __global__ __launch_bounds__(256) void k_fset_probe(Src src, uint64_t n, const RangedFilter* __restrict__ filters,
                                                     uint32_t nfilt, uint64_t* __restrict__ out) {
     __shared__ RangedFilter fl[64];
+    __shared__ Pfx16 blo[64], bhi[64];
     for (uint32_t f = threadIdx.x; f < nfilt; f += blockDim.x) fl[f] = filters[f];
+    __syncthreads();
+    stage_bounds(fl, nfilt, blo, bhi);
     __syncthreads();
     const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
         const H128 h = src.hash(i);
         const uint8_t* kp = src.bytes(i);
         const uint64_t kl = src.key_len(i);
+        const Pfx16 kx = prefix16(kp, kl);
         uint64_t m = 0;
         // Positions of the last (num_bits, k <= 8) walked: the store's SST
         // filters all share one sizing (builder.rs:51,74), so one walk serves
@@ -173,7 +219,8 @@ __global__ __launch_bounds__(256) void k_fset_probe(Src src, uint64_t n, const R
         uint32_t cnb = 0, ck = 0;
         for (uint32_t f = 0; f < nfilt; f++) {
             const RangedFilter& R = fl[f];
-            if (key_cmp(kp, kl, R.lo, R.lo_len) < 0 || key_cmp(kp, kl, R.hi, R.hi_len) > 0) continue;
+            if (cmp_pfx(kx, kp, kl, blo[f], R.lo, R.lo_len) < 0 || cmp_pfx(kx, kp, kl, bhi[f], R.hi, R.hi_len) > 0)
+                continue;
             bool hit = true;
             if (R.f.k && R.f.k <= 8) {
                 if (R.f.num_bits != cnb || R.f.k != ck) {
@@ -218,9 +265,11 @@ __global__ __launch_bounds__(256) void k_fset_sliced(Src src, uint64_t n, const 
                                                      uint32_t nfilt, uint32_t k_, uint64_t* __restrict__ out) {
     extern __shared__ __align__(16) uint8_t smem_raw[];
     __shared__ RangedFilter fl[64];
+    __shared__ Pfx16 blo[64], bhi[64];
     T* table = reinterpret_cast<T*>(smem_raw);
     for (uint32_t f = threadIdx.x; f < nfilt; f += blockDim.x) fl[f] = filters[f];
     __syncthreads();
+    stage_bounds(fl, nfilt, blo, bhi);
     const uint32_t num_bits = fl[0].f.num_bits;
     const Mod32 md = fl[0].f.md;
     const uint32_t nw32 = (num_bits + 31) / 32;  // num_bits <= 2^19 here: no wrap
@@ -242,10 +291,12 @@ __global__ __launch_bounds__(256) void k_fset_sliced(Src src, uint64_t n, const 
         const H128 h = src.hash(i);
         const uint8_t* kp = src.bytes(i);
         const uint64_t kl = src.key_len(i);
+        const Pfx16 kx = prefix16(kp, kl);
         T m = 0;
         for (uint32_t f = 0; f < nfilt; f++) {
             const RangedFilter& R = fl[f];
-            if (key_cmp(kp, kl, R.lo, R.lo_len) >= 0 && key_cmp(kp, kl, R.hi, R.hi_len) <= 0) m |= (T)((T)1 << f);
+            if (cmp_pfx(kx, kp, kl, blo[f], R.lo, R.lo_len) >= 0 && cmp_pfx(kx, kp, kl, bhi[f], R.hi, R.hi_len) <= 0)
+                m |= (T)((T)1 << f);
         }
         if (m) {
             Walk32 pw(md, h.lo, h.hi);

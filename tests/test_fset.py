@@ -209,3 +209,29 @@ def test_fset_same_sized_sliced_table_widths(oracle, ntab, fpr):
     assert [int(x) for x in got] == expected_masks(oracle, tables, [bytes(r) for r in q])
     fs.close()
     ctx.close()
+
+
+@pytest.mark.gpu
+def test_fset_bounds_sharing_16_byte_prefixes(oracle):
+    # range checks first order by the zero-padded 16-byte prefixes; ties fall
+    # to lengths (both <= 16 B) or the full byte compare
+    ctx = lsmbloom.Context(0)
+    fs = FilterSet(ctx)
+    P = b"0123456789abcdef"
+    nb, k = lsmbloom.params(64, 0.01)
+    bounds = [(P, P + b"\x00"), (P + b"a", P + b"m"), (P[:15], P), (P[:8] + b"\x00" * 8, P[:8] + b"\x00" * 9),
+              (b"", P[:3]), (P + b"zz" * 10, P + b"zz" * 10 + b"\x01")]
+    q = [P, P[:15], P + b"\x00", P + b"\x00\x00", P + b"a", P + b"m", P + b"ma", P + b"b" * 30, P[:14],
+         P[:8] + b"\x00" * 7, P[:8] + b"\x00" * 8, P[:8] + b"\x00" * 9, P[:8] + b"\x00" * 10, b"", P[:3],
+         P[:3] + b"\x00", P + b"zz" * 10, P + b"zz" * 10 + b"\x00", P + b"zz" * 10 + b"\x01\x00", P[:8]]
+    tables = {}
+    for lo, hi in bounds:
+        w = np.zeros(lsmbloom.num_words(nb), np.uint64)
+        for key in q:
+            oracle.insert(w, nb, k, key)  # every query a member: the range decides
+        s = fs.add_filter(BloomFilter(w, k, nb), lo, hi)
+        tables[s] = (w, nb, k, lo, hi)
+    got = fs.probe_keys(q)
+    assert [int(x) for x in got] == expected_masks(oracle, tables, q)
+    fs.close()
+    ctx.close()
