@@ -272,6 +272,8 @@ __global__ __launch_bounds__(256) void k_fset_sliced(Src src, uint64_t n, const 
     stage_bounds(fl, nfilt, blo, bhi);
     const uint32_t num_bits = fl[0].f.num_bits;
     const Mod32 md = fl[0].f.md;
+    bool ident = true;  // slots 0..nfilt-1 all live: table bit f is output bit f
+    for (uint32_t f = 0; f < nfilt; f++) ident = ident && fl[f].f.out_bit == f;
     const uint32_t nw32 = (num_bits + 31) / 32;  // num_bits <= 2^19 here: no wrap
     for (uint32_t w = threadIdx.x; w < nw32; w += blockDim.x) {
         T acc[32];
@@ -313,9 +315,12 @@ __global__ __launch_bounds__(256) void k_fset_sliced(Src src, uint64_t n, const 
                 }
             }
         }
-        uint64_t o = 0;
-        for (uint32_t f = 0; f < nfilt; f++)
-            if ((m >> f) & 1) o |= 1ull << fl[f].f.out_bit;
+        uint64_t o = (uint64_t)m;
+        if (!ident) {
+            o = 0;
+            for (uint32_t f = 0; f < nfilt; f++)
+                if ((m >> f) & 1) o |= 1ull << fl[f].f.out_bit;
+        }
         out[i] = o;
     }
 }
