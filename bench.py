@@ -1,19 +1,23 @@
 #!/usr/bin/env python3
 """bench.py — BASELINE metric: Bloom build (+ batched probe), Mkeys/s, device-resident.
 
-A step = one device-resident build of a fresh filter over this rank's batch of
-synthetic 16-byte keys (BASELINE configs[1] = C2 at N=1: 100 M keys into
-BloomFilter::new(1e8, 0.01) -> 956 715 292 bits, k = 7), i.e. zero the words,
-hash every key, set its 7 bits — and, for N > 1 GPUs, the bitwise-OR allreduce
-that merges the ranks' partial filters (RCCL has no BOR op: all_to_all
-reduce-scatter + native OR kernel + all_gather).  Weak scaling: each rank owns
---keys-per-gpu keys of one global run; the filter is sized for the global run
-(for N >= 5 that saturates at 2^32-1 bits, the C5 filter, src/bloom/mod.rs:49).
+A step = one device-resident build of a fresh filter over this rank's shard of
+synthetic 16-byte keys, i.e. zero the words, hash every key, set its 7 bits —
+and, for N > 1 GPUs, the bitwise-OR allreduce that merges the ranks' partial
+filters (RCCL has no BOR op: all_to_all reduce-scatter + native OR kernel +
+all_gather).
+  N = 1: C2 (BASELINE configs[1]): 100 M keys into BloomFilter::new(1e8, 0.01)
+         -> 956 715 292 bits, k = 7.
+  N > 1: C5 (configs[4]): 1e9 keys split over the N ranks (strong scaling) into
+         new(1e9, 0.01) = 2^32-1 bits (the saturated u32, src/bloom/mod.rs:49).
+`--gpus N` launched without torchrun starts the N rank processes itself.
 
 Also reported (extra keys on the same JSON line):
   probe        C3: 10 M 16-B lookup keys x 8 SSTable filters (new(1000, 0.01)), Mkeys/s
   roofline     the build kernels vs 8 TB/s HBM, algorithmic bytes per build
-  cpu_baseline the CPU oracle (C restatement of src/bloom, "port") on a bounded sample
+  cpu_baseline the CPU oracle (C restatement of src/bloom, "port") on a bounded sample,
+               and C1 (configs[0]) build + probe, 1 thread and all cores
+  c2_exact_10_bits_per_key  the C2 keys into num_bits = 10 n, k = 7
 """
 import argparse
 import json
@@ -35,7 +39,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--keys-per-gpu", type=int, default=100_000_000)
+    ap.add_argument("--global-keys", type=int, default=0,
+                    help="keys of the whole run, split over the ranks (default: 1e8 = C2 at N=1, 1e9 = C5 at N>1)")
+    ap.add_argument("--keys-per-gpu", type=int, default=0,
+                    help="weak scaling instead: this many keys per rank (overrides --global-keys)")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
     ap.add_argument("--probe-keys", type=int, default=10_000_000)
     ap.add_argument("--probe-filters", type=int, default=8)
     ap.add_argument("--no-probe", action="store_true")
@@ -44,14 +52,59 @@ def parse():
     ap.add_argument("--verify", action="store_true", help="check the built filter against the oracle")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory end-to-end measurement")
     ap.add_argument("--no-varlen", action="store_true", help="skip the C4 variable-length build leg")
+    ap.add_argument("--no-exact10", action="store_true", help="skip the C2 exact 10 bits/key leg")
     ap.add_argument("--varlen-keys", type=int, default=100_000_000)
-    ap.add_argument("--filter-keys", type=int, default=0, help="size the filter for this many keys (default: all ranks' keys)")
+    ap.add_argument("--filter-keys", type=int, default=0, help="size the filter for this many keys (default: the global run)")
     return ap.parse_args()
 
 
+def spawn_ranks(args):
+    """`bench.py --gpus N` without a launcher: start N rank processes (one per
+    GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in their env) and wait for them.
+    Nothing in this parent touches a GPU.  Rank 0 prints the JSON line; the
+    exit code is the first failing rank's (the others are then stopped)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            r = p.poll()
+            if r is None:
+                continue
+            alive.remove(p)
+            if r != 0 and rc == 0:
+                rc = r if r > 0 else 1
+                for q in alive:
+                    q.terminate()
+        time.sleep(0.1)
+    return rc
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(num_bits, k, budget_s):
-    """Oracle (C restatement of src/bloom, single thread) building the C2-size
-    filter from the first S keys of the same workload, S grown until ~budget_s."""
+    """Oracle (C restatement of src/bloom) on the box's host cores, reported
+    beside the GPU numbers: the C2-size filter built from the
+    first S keys of the same workload (S grown until ~budget_s, 1 thread, and
+    all cores with atomic fetch_or), and C1 (configs[0]): build + probe of
+    100 k 16-B keys, 1 thread and all cores."""
     import numpy as np
     import oracle_ct
     orc = oracle_ct.load()
@@ -64,11 +117,11 @@ def cpu_baseline(num_bits, k, budget_s):
         orc.build_fixed(keys, 16, num_bits, k, words=words)
         t_used += time.perf_counter() - t0
         done += chunk
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
     st = {"value": round(done / t_used / 1e6, 3), "unit": "Mkeys/s", "cores": 1, "kind": "port",
+          "cpu": cpu_model(), "host_threads_available": threads,
           "sample": "first %d keys of the C2 workload into the full C2 filter (%d bits, k=%d), "
                     "1 thread, oracle/bloom_oracle.c -O3" % (done, num_bits, k)}
-    # all-cores variant (the box's CPU share: at most 16 threads)
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
     words[:] = 0
     n_mt = min(done * threads, 20_000_000)
     keys = orc.key16(SEED_MEMBERS, 0, n_mt)
@@ -77,44 +130,113 @@ def cpu_baseline(num_bits, k, budget_s):
     dt = time.perf_counter() - t0
     st["multi_thread"] = {"value": round(n_mt / dt / 1e6, 3), "cores": threads,
                           "sample": "first %d keys, atomic fetch_or" % n_mt}
+    st["c1"] = cpu_c1(orc, threads)
     return st
+
+
+def cpu_c1(orc, threads, reps=20):
+    """C1 (BASELINE configs[0]): BloomFilter::new(100000, 0.01) built from 100 k
+    key16 members, then 100 k members + 100 k non-members probed; the oracle
+    on 1 thread and on `threads` threads (probe: key chunks per thread, the
+    ctypes calls release the GIL)."""
+    import numpy as np
+    from concurrent.futures import ThreadPoolExecutor
+    n = 100_000
+    nb, k = orc.params(n, 0.01)
+    mem = orc.key16(SEED_MEMBERS, 0, n)
+    non = orc.key16(SEED_FRESH, 0, n)
+    q = np.concatenate([mem, non])
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ref = orc.build_fixed(mem, 16, nb, k)
+    tb1 = (time.perf_counter() - t0) / reps
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ans = orc.probe([(ref, nb, k)], q, key_len=16)
+    tp1 = (time.perf_counter() - t0) / reps
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        orc.build_fixed_mt(mem, 16, nb, k, threads)
+    tbm = (time.perf_counter() - t0) / reps
+    parts = np.array_split(q, threads)
+    with ThreadPoolExecutor(threads) as ex:
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            list(ex.map(lambda p: orc.probe([(ref, nb, k)], p, key_len=16), parts))
+        tpm = (time.perf_counter() - t0) / reps
+    fp = int(ans[n:, 0].sum())
+    return {"workload": "C1 (configs[0]): build new(100000, 0.01) (%d bits, k=%d) from 100000 key16 members; "
+                        "probe 100000 members + 100000 non-members" % (nb, k),
+            "build_1t": {"ms": round(tb1 * 1e3, 3), "value": round(n / tb1 / 1e6, 2), "unit": "Mkeys/s"},
+            "probe_1t": {"ms": round(tp1 * 1e3, 3), "value": round(2 * n / tp1 / 1e6, 2), "unit": "Mkeys/s"},
+            "build_mt": {"ms": round(tbm * 1e3, 3), "value": round(n / tbm / 1e6, 2), "unit": "Mkeys/s",
+                         "cores": threads},
+            "probe_mt": {"ms": round(tpm * 1e3, 3), "value": round(2 * n / tpm / 1e6, 2), "unit": "Mkeys/s",
+                         "cores": threads},
+            "members_all_hit": bool(ans[:n, 0].all()), "non_member_fp": fp}
+
+
+def shard(total, world, rank):
+    return total * rank // world, total * (rank + 1) // world
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world), file=sys.stderr)
+        sys.exit(2)
     import numpy as np
     import torch
     import torch.distributed as dist
 
     import lsmbloom
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-    ctx = lsmbloom.Context(local)
-    stream = torch.cuda.current_stream(dev)
-
-    npg = args.keys_per_gpu
-    total = npg * world
-    # --filter-keys: size the filter for a larger global run than this job's
-    # keys (rehearses the per-GPU build of an N-GPU run on one GPU; C5's
-    # 1e9-key filter saturates at 2^32-1 bits).  Reported in config.
-    nb, k = lsmbloom.params(args.filter_keys or total, 0.01)
-    nw = lsmbloom.num_words(nb)
-    keys = torch.empty((npg, 16), dtype=torch.uint8, device=dev)
-    ctx.gen_key16_dev(SEED_MEMBERS, rank * npg, npg, keys)
-    words = torch.zeros(nw, dtype=torch.int64, device=dev)
     from lsmbloom import dist as ldist
 
-    def step():
+    ndev = torch.cuda.device_count()
+    if world > 1 and args.backend == "nccl" and world > ndev:
+        print("bench.py: %d RCCL ranks need %d GPUs, %d visible" % (world, world, ndev), file=sys.stderr)
+        sys.exit(2)
+    dev = torch.device("cuda", local % max(1, ndev))
+    torch.cuda.set_device(dev)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
+    ctx = lsmbloom.Context(dev.index)
+
+    # Workload.  N = 1: C2 (configs[1]), 100 M keys into new(1e8, 0.01).
+    # N > 1: C5 (configs[4]), 1e9 keys split over the ranks (strong scaling),
+    # filter new(1e9, 0.01) = 2^32-1 bits.  --keys-per-gpu: weak scaling.
+    if args.keys_per_gpu:
+        total = args.keys_per_gpu * world
+        lo, hi = rank * args.keys_per_gpu, (rank + 1) * args.keys_per_gpu
+        scaling = "weak"
+    else:
+        total = args.global_keys or (100_000_000 if world == 1 else 1_000_000_000)
+        lo, hi = shard(total, world, rank)
+        scaling = "strong"
+    npg = hi - lo
+    nmax = max(shard(total, world, r)[1] - shard(total, world, r)[0] for r in range(world))
+    nb, k = lsmbloom.params(args.filter_keys or total, 0.01)
+    nw = lsmbloom.num_words(nb)
+    cfg_name = {100_000_000: "C2 (configs[1])", 1_000_000_000: "C5 (configs[4])"}.get(total, "custom")
+    keys = torch.empty((npg, 16), dtype=torch.uint8, device=dev)
+    ctx.gen_key16_dev(SEED_MEMBERS, lo, npg, keys)
+    words = torch.zeros(nw, dtype=torch.int64, device=dev)
+    host_coll = world > 1 and args.backend != "nccl"
+
+    def build():
         words.zero_()
         ctx.build_fixed_dev(keys, 16, npg, nb, k, words)
+
+    def allreduce():
         if world > 1:
             ldist.or_allreduce_(words, ctx=ctx)
 
@@ -123,73 +245,102 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
 
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device="cpu" if host_coll else dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
     ctx.set_timing(False)  # no timing markers between the kernels of a timed step
     for _ in range(args.warmup):
-        step()
+        build()
+        allreduce()
     barrier()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for e0, e1, e2 in ev:
+        e0.record()
+        build()
+        e1.record()
+        allreduce()
+        e2.record()
     barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = max_over_ranks(time.perf_counter() - t0)
     ms = dt / args.steps * 1e3
     value = total * args.steps / dt / 1e6
+    build_ms = max_over_ranks(sum(a.elapsed_time(b) for a, b, _ in ev) / args.steps)
+    coll_ms = max_over_ranks(sum(b.elapsed_time(c) for _, b, c in ev) / args.steps)
 
     # per-kernel times (HIP events on the build stream), averaged over `steps` builds
     ctx.set_timing(True)
     kt = np.zeros(3)
     for _ in range(args.steps):
-        words.zero_()
-        ctx.build_fixed_dev(keys, 16, npg, nb, k, words)
+        build()
         ctx.sync()
         torch.cuda.synchronize(dev)
         kt += np.array(ctx.last_build_ms())
     kt /= args.steps
-    strategy = lsmbloom.build_strategy(nb, npg)
+    ctx.set_timing(False)
+    strategy = lsmbloom.build_strategy(nb, npg, k)
     alg_bytes = 16 * npg + 8 * nw
     achieved = alg_bytes / (kt[0] * 1e-3) / 1e9
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
             "kernel": "build (%s: k_bin + k_apply)" % strategy,
-            "algorithmic_bytes": alg_bytes, "kernel_ms": round(float(kt[0]), 4),
-            "pass_a_ms": round(float(kt[1]), 4), "pass_b_ms": round(float(kt[2]), 4)}
+            "algorithmic_bytes": alg_bytes, "algorithmic_bytes_per_key": round(alg_bytes / npg, 3),
+            "kernel_ms": round(float(kt[0]), 4), "pass_a_ms": round(float(kt[1]), 4),
+            "pass_b_ms": round(float(kt[2]), 4)}
 
     out = {"metric": "bloom build + batched probe, Mkeys/s device-resident, at 1/2/4/8 MI355X",
            "value": round(value, 2), "unit": "Mkeys/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
-           "scaling": "weak", "vs_baseline": None, "dtype": "u8/u64 (XXH3-128 + bit OR)",
+           "scaling": scaling, "vs_baseline": None, "dtype": "u8/u64 (XXH3-128 + bit OR)",
            "data": "synthetic key16(0x5EED0001, i) = splitmix64 stream, generated on device",
-           "config": {"workload": "C2 (configs[1]): build BloomFilter::new(%d, 0.01) from %d 16-B keys per GPU"
-                                  % (total, npg),
-                      "keys_per_gpu": npg, "global_keys": total, "num_bits": nb, "k": k,
-                      "filter_bytes": 8 * nw, "strategy": strategy, "parallelism": "dp%d" % world}}
+           "config": {"workload": "%s: build BloomFilter::new(%d, 0.01) from %d 16-B keys, %d per GPU"
+                                  % (cfg_name, args.filter_keys or total, total, nmax),
+                      "keys_per_gpu": nmax, "global_keys": total, "num_bits": nb, "k": k,
+                      "filter_bytes": 8 * nw, "strategy": strategy, "scaling": scaling,
+                      "parallelism": "dp%d" % world}}
     if args.filter_keys:
         out["config"]["filter_sized_for_keys"] = args.filter_keys
     out["roofline"] = roof
-
     if world > 1:
-        # Multi-GPU self-check (outside the timed region): one more sharded
-        # step (build + OR-allreduce); rank 0 then rebuilds the whole global
-        # key set alone, 100 M keys at a time, and compares every word.  OR is
-        # associative and idempotent, so the merged filter must be identical.
-        step()
+        moved = 2 * (world - 1) / world * 8 * nw
+        out["config"]["backend"] = args.backend
+        out["step_split"] = {"build_ms": round(build_ms, 4), "or_allreduce_ms": round(coll_ms, 4),
+                             "what": "per step, slowest rank: zero + device build / bitwise-OR allreduce "
+                                     "(all_to_all reduce-scatter + native OR kernel + all_gather)",
+                             "or_allreduce_bytes_per_gpu": int(moved),
+                             "or_allreduce_GBs_per_gpu": round(moved / (coll_ms * 1e-3) / 1e9, 1) if coll_ms else None}
+        # Self-check (outside the timed region): one more sharded step; rank 0
+        # then rebuilds the whole global key set alone, shard by shard, and
+        # compares every word.  Its build time is the 1-GPU time of this same
+        # workload (C5 on one GPU), for the strong-scaling curve.
+        build()
+        allreduce()
         torch.cuda.synchronize(dev)
         if rank == 0:
             try:
                 ref = torch.zeros_like(words)
-                for first in range(0, total, npg):
-                    m = min(npg, total - first)
-                    ctx.gen_key16_dev(SEED_MEMBERS, first, m, keys[:m])
-                    ctx.build_fixed_dev(keys[:m], 16, m, nb, k, ref)
+                buf = torch.empty((nmax, 16), dtype=torch.uint8, device=dev)
+                one_ms = 0.0
+                for r in range(world):
+                    a, b = shard(total, world, r) if scaling == "strong" else (r * npg, (r + 1) * npg)
+                    ctx.gen_key16_dev(SEED_MEMBERS, a, b - a, buf[: b - a])
+                    s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    s0.record()
+                    ctx.build_fixed_dev(buf[: b - a], 16, b - a, nb, k, ref)
+                    s1.record()
+                    torch.cuda.synchronize(dev)
+                    one_ms += s0.elapsed_time(s1)
                 ctx.sync()
-                torch.cuda.synchronize(dev)
                 out["multi_gpu_merged_equals_single_gpu_build"] = bool(torch.equal(ref, words))
-                del ref
-                ctx.gen_key16_dev(SEED_MEMBERS, rank * npg, npg, keys)  # this rank's shard again
+                out["single_gpu_same_workload"] = {
+                    "what": "rank 0 alone builds all %d keys into the same filter (build kernels only)" % total,
+                    "ms": round(one_ms, 3), "value": round(total / (one_ms * 1e-3) / 1e6, 2), "unit": "Mkeys/s"}
+                del ref, buf
             except Exception as e:  # report, never lose the bench line
                 out["multi_gpu_check_error"] = repr(e)[:200]
         dist.barrier()
@@ -202,7 +353,9 @@ def main():
         out["verified_bit_exact"] = bool(np.array_equal(words.cpu().numpy().view(np.uint64), ref))
 
     if not args.no_probe:
-        out["probe"] = bench_probe(ctx, dev, args)
+        out["probe"] = bench_probe(ctx, dev, args, world, rank, max_over_ranks)
+    if world == 1 and not args.no_exact10:
+        out["c2_exact_10_bits_per_key"] = bench_exact10(ctx, keys, npg)
     if not args.no_e2e and rank == 0 and world == 1:
         out["e2e"] = bench_e2e(ctx, keys, npg, nb, k)
 
@@ -212,9 +365,12 @@ def main():
     if not args.no_varlen and world == 1:
         out["varlen"] = bench_varlen(ctx, dev, args)
     tr = committed_traffic()
-    if tr:
-        out["roofline"]["traffic"] = tr["bytes"]
+    if tr and world == 1 and total == 100_000_000 and not args.filter_keys:
         out["roofline"]["traffic_source"] = tr["source"]
+        if tr["fresh"]:
+            out["roofline"]["traffic"] = tr["bytes"]
+        else:
+            out["roofline"]["traffic_stale"] = "kernel sources changed since %s was profiled" % tr["source"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(nb, k, args.cpu_seconds)
         out["cpu_baseline"]["gpu_over_cpu_1thread"] = round(value / out["cpu_baseline"]["value"], 1)
@@ -223,6 +379,43 @@ def main():
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_exact10(ctx, keys, n, reps=10):
+    """C2's exact 10-bits-per-key variant: num_bits =
+    10 n, k = 7 (reachable in the reference through deserialize of a zeroed
+    header + inserts, src/bloom/mod.rs:123-168), same keys, device build."""
+    import numpy as np
+    import torch
+
+    import lsmbloom
+    nb, k = 10 * n, 7
+    if nb >= 2 ** 32:
+        return {"skipped": "10 n >= 2^32 bits is not representable (num_bits is u32)"}
+    w = torch.zeros(lsmbloom.num_words(nb), dtype=torch.int64, device=keys.device)
+    ctx.set_timing(True)
+    kt = np.zeros(3)
+    for i in range(reps + 2):
+        w.zero_()
+        ctx.build_fixed_dev(keys, 16, n, nb, k, w)
+        ctx.sync()
+        torch.cuda.synchronize(keys.device)
+        if i >= 2:
+            kt += np.array(ctx.last_build_ms())
+    ctx.set_timing(False)
+    kt /= reps
+    alg = 16 * n + 8 * lsmbloom.num_words(nb)
+    fill = int(np.bitwise_count(w.cpu().numpy().view(np.uint64)).sum(dtype=np.uint64))
+    res = {"workload": "C2 exact: %d 16-B keys into num_bits = 10 n = %d, k = 7" % (n, nb),
+           "value": round(n / (kt[0] * 1e-3) / 1e6, 1), "unit": "Mkeys/s", "kernel_ms": round(float(kt[0]), 4),
+           "pass_a_ms": round(float(kt[1]), 4), "pass_b_ms": round(float(kt[2]), 4),
+           "strategy": lsmbloom.build_strategy(nb, n, k),
+           "frac": round(alg / (kt[0] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    # expected fill of an ideal filter: 1 - exp(-k n / m)
+    res["fill_ratio"] = round(fill / nb, 5)
+    res["fill_ratio_expected"] = round(1 - float(np.exp(-k * n / nb)), 5)
+    del w
+    return res
 
 
 def bench_e2e(ctx, keys, n, nb, k, reps=3):
@@ -259,26 +452,41 @@ def bench_e2e(ctx, keys, n, nb, k, reps=3):
     res["unit"] = "Mkeys/s"
     # SST-sized flushes: one lsmb_build_block call per table, sized like
     # SSTableBuilder::with_estimated_keys (builder.rs:74); latency per call
-    # (H2D, kernels, D2H, sync) next to the 1-thread CPU oracle on the same keys.
+    # (H2D, kernels, D2H, sync) next to the 1-thread CPU oracle on the same
+    # keys.  Each size runs twice: through the default dispatch ("path": the
+    # library's host loop at or below lsmb_host_max_keys, else the GPU) and
+    # forced onto the GPU (threshold 0): the crossover sets the threshold.
     import oracle_ct
     orc = oracle_ct.load()
     small = []
-    for m in (1000, 100_000, 1_000_000):
-        nb_m, k_m = lsmbloom.params(m, 0.01)
-        ks = np.ascontiguousarray(host[: m * 16])
-        blk = np.empty(lsmbloom.serialized_size(nb_m), dtype=np.uint8)
+    thr = lsmbloom.host_max_keys()
+
+    def lat(ks, nb_m, k_m, blk, reps=20):
         ctx.build_block(ks, nb_m, k_m, key_len=16, out=blk)
         ts = []
-        for _ in range(20):
+        for _ in range(reps):
             t0 = time.perf_counter()
             ctx.build_block(ks, nb_m, k_m, key_len=16, out=blk)
             ts.append(time.perf_counter() - t0)
+        return float(np.median(ts)) * 1e3
+
+    for m in (250, 500, 1000, 2000, 4000, 8000, 100_000, 1_000_000):
+        nb_m, k_m = lsmbloom.params(m, 0.01)
+        ks = np.ascontiguousarray(host[: m * 16])
+        blk = np.empty(lsmbloom.serialized_size(nb_m), dtype=np.uint8)
+        t_default = lat(ks, nb_m, k_m, blk)
+        lsmbloom.set_host_max_keys(0)
+        blk_gpu = np.empty_like(blk)
+        t_gpu = lat(ks, nb_m, k_m, blk_gpu)
+        lsmbloom.set_host_max_keys(thr)
         t0 = time.perf_counter()
         ref = orc.build_fixed(ks.reshape(m, 16), 16, nb_m, k_m)
         tc = time.perf_counter() - t0
-        small.append({"keys": m, "strategy": lsmbloom.build_strategy(nb_m, m),
-                      "gpu_ms": round(float(np.median(ts)) * 1e3, 3), "cpu_oracle_1t_ms": round(tc * 1e3, 3),
-                      "bit_exact": bool(np.array_equal(np.frombuffer(blk[12:].tobytes(), dtype=np.uint64), ref))})
+        small.append({"keys": m, "path": "host" if m <= thr else lsmbloom.build_strategy(nb_m, m, k_m),
+                      "ms": round(t_default, 4), "gpu_ms": round(t_gpu, 4), "cpu_oracle_1t_ms": round(tc * 1e3, 4),
+                      "bit_exact": bool(np.array_equal(np.frombuffer(blk[12:].tobytes(), dtype=np.uint64), ref)
+                                        and np.array_equal(blk, blk_gpu))})
+    res["host_max_keys"] = thr
     res["sst_flush_latency"] = small
     return res
 
@@ -334,26 +542,46 @@ def bench_varlen(ctx, dev, args):
     return res
 
 
+BUILD_SOURCES = ("storage-engine_amd/csrc/bloom_build.hip", "storage-engine_amd/csrc/kernels.hpp",
+                 "storage-engine_amd/csrc/bloom_math.hpp", "storage-engine_amd/csrc/xxh3.hpp",
+                 "storage-engine_amd/csrc/keysrc.hpp")
+
+
+def build_sources_sha():
+    """sha256 over the C2 build kernels' sources: stamps profiles/traffic.json."""
+    import hashlib
+    h = hashlib.sha256()
+    for p in BUILD_SOURCES:
+        with open(os.path.join(ROOT, p), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def committed_traffic():
     """HBM bytes per C2 build from the committed rocprofv3 PMC summary
     (profiles/traffic.json, written by tools/prof_summary.py --json from separate
     FETCH_SIZE / WRITE_SIZE passes of this bench; FETCH_SIZE doubled per the
-    gfx950 note in MI355X_MICROARCH.md).  None if absent."""
+    gfx950 note in MI355X_MICROARCH.md).  `fresh` is False when the build
+    kernels' sources changed since that profile (its stamped sha differs)."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(p):
         return None
     t = json.load(open(p))
-    return {"bytes": t.get("build_bytes"), "source": "%s (%s)" % (os.path.relpath(p, ROOT), t.get("profile"))}
+    return {"bytes": t.get("build_bytes"), "source": "%s (%s)" % (os.path.relpath(p, ROOT), t.get("profile")),
+            "fresh": t.get("kernel_src_sha") == build_sources_sha()}
 
 
-def bench_probe(ctx, dev, args):
+def bench_probe(ctx, dev, args, world=1, rank=0, max_over_ranks=lambda x: x):
     """C3: Q lookup keys (50% members drawn across the F filters, 50% fresh)
-    against F per-SSTable filters sized like SSTableBuilder::new (1000 keys, 0.01)."""
+    against F per-SSTable filters sized like SSTableBuilder::new (1000 keys, 0.01).
+    N > 1: the filters are replicated and the queries partitioned (no
+    collective); the rate counts all ranks' queries over the slowest rank."""
     import numpy as np
     import torch
 
     import lsmbloom
-    F, Q = args.probe_filters, args.probe_keys
+    F, Q_all = args.probe_filters, args.probe_keys
+    Q = Q_all // world
     nb, k = lsmbloom.params(1000, 0.01)
     nw = lsmbloom.num_words(nb)
     filt = []
@@ -379,12 +607,12 @@ def bench_probe(ctx, dev, args):
         ctx.probe_dev(filt, q, Q, out, key_len=16)
     en.record()
     torch.cuda.synchronize(dev)
-    ms = st.elapsed_time(en) / args.steps
+    ms = max_over_ranks(st.elapsed_time(en) / args.steps)
     alg = Q * 16 + Q * out.shape[1] + F * (12 + 8 * nw)
     hits = int((out[: Q // 2] != 0).all(dim=1).sum().item())
-    res = {"workload": "C3 (configs[2]): %d 16-B keys x %d filters new(1000, 0.01) (%d bits, k=%d)"
-                       % (Q, F, nb, k),
-           "value": round(Q / (ms * 1e-3) / 1e6, 2), "unit": "Mkeys/s", "ms": round(ms, 4),
+    res = {"workload": "C3 (configs[2]): %d 16-B keys x %d filters new(1000, 0.01) (%d bits, k=%d)%s"
+                       % (Q_all, F, nb, k, ", %d per GPU" % Q if world > 1 else ""),
+           "value": round(Q * world / (ms * 1e-3) / 1e6, 2), "unit": "Mkeys/s", "ms": round(ms, 4),
            "achieved_GBs": round(alg / (ms * 1e-3) / 1e9, 1), "member_rows_all_hit": hits == Q // 2}
     # The same batch through the device-resident filter set (lsmb_fset): per
     # key and SSTable, min_key <= key <= max_key && may_contain — the checks
@@ -405,11 +633,11 @@ def bench_probe(ctx, dev, args):
         fs.probe_dev(q, Q, fout, key_len=16)
     en.record()
     torch.cuda.synchronize(dev)
-    fms = st.elapsed_time(en) / args.steps
+    fms = max_over_ranks(st.elapsed_time(en) / args.steps)
     # a member row's own table must answer 1 (range and bloom); here sel // 1000
     own = (fout[: Q // 2] >> torch.tensor(slots, device=dev)[sel // 1000]) & 1
     res["fset"] = {"what": "lsmb_fset_probe_dev: range pre-check + bloom, %d tables, u64 mask per key" % F,
-                   "value": round(Q / (fms * 1e-3) / 1e6, 2), "unit": "Mkeys/s", "ms": round(fms, 4),
+                   "value": round(Q * world / (fms * 1e-3) / 1e6, 2), "unit": "Mkeys/s", "ms": round(fms, 4),
                    "member_rows_own_table_hit": bool(own.all().item())}
     fs.close()
     return res

@@ -19,8 +19,13 @@
  *     ceil(num_bits/64) little-endian u64, bit p = word p/64, bit p%64.
  *   - Batched build entry points OR-ACCUMULATE into `words` (existing bits are
  *     kept), so a build after insert()s, or a merge of shard partials, is exact.
- *   - Batched entry points run on the GPU only.  With no usable gfx950 device,
- *     lsmb_open fails with LSMB_ENODEV: there is no silent CPU fallback.
+ *   - Batched entry points run on the GPU.  With no usable gfx950 device,
+ *     lsmb_open fails with LSMB_ENODEV: there is no silent CPU fallback.  The
+ *     one host path is deliberate and size-bounded: host-memory builds of at
+ *     most lsmb_host_max_keys() keys (an SST flush of the reference's default
+ *     1 000-key sizing, src/sstable/builder.rs:51,74) run the library's own
+ *     per-key loop, where a device round trip costs more than the whole build;
+ *     for those ctx may be NULL, so the store works on a host without a GPU.
  *   - Thread safety: a context may be used from one thread at a time; distinct
  *     contexts (e.g. flush + background compaction, src/compaction/scheduler.rs:37)
  *     may run concurrently.  Stateless functions are always thread safe.
@@ -42,7 +47,7 @@ extern "C" {
 #define LSMB_ECORRUPT (-4) /* serialized filter fails validation               */
 #define LSMB_ENOMEM (-5)   /* device or pinned-host allocation failed          */
 
-#define LSMB_ABI_VERSION 3
+#define LSMB_ABI_VERSION 4
 
 typedef struct lsmb_ctx lsmb_ctx; /* one GPU: stream, events, scratch arenas */
 
@@ -108,7 +113,14 @@ int lsmb_sync(lsmb_ctx* ctx);
 /* ---- batched build (BloomFilterBuilder::add_key loop + build) ------------ */
 /* Host-memory entry points: the keys go up in chunks through two device
  * staging slots (chunk i+1's H2D overlaps chunk i's kernels), the build runs on
- * the GPU, the words come back (OR-accumulated into `words`).  Synchronous. */
+ * the GPU, the words come back (OR-accumulated into `words`).  Synchronous.
+ * n <= lsmb_host_max_keys(): the library's host loop builds the same bits with
+ * no device round trip, and ctx may be NULL (above it, NULL is LSMB_EINVAL). */
+
+/* Size threshold of the host path (default 2048 keys, env LSMB_HOST_MAX_KEYS;
+ * 0 sends every build to the GPU).  The bits never depend on it. */
+uint64_t lsmb_host_max_keys(void);
+void lsmb_set_host_max_keys(uint64_t n);
 
 /* n keys of key_len bytes each, packed back to back (key i at keys + i*key_len). */
 int lsmb_build_fixed(lsmb_ctx* ctx, const uint8_t* keys, uint32_t key_len, uint64_t n,
@@ -177,6 +189,48 @@ int lsmb_gen_key16_dev(lsmb_ctx* ctx, uint64_t seed, uint64_t first, uint64_t n,
 int lsmb_gen_splitmix_dev(lsmb_ctx* ctx, uint64_t seed, uint64_t first, uint64_t n, uint32_t mod,
                           uint32_t add, void* d_out, void* stream);
 
+/* ---- one process, several GPUs (sharded build) -------------------------- */
+/* When one flush / compaction run is large (src/db/mod.rs:377-383,
+ * src/compaction/scheduler.rs:150-158, both feeding SSTableBuilder::add,
+ * src/sstable/builder.rs:93), lsmb_multi splits its keys into G contiguous
+ * shards, builds a full-size partial filter per shard on its own GPU and merges
+ * the partials with a bitwise-OR reduce-scatter done by peer loads over xGMI.
+ * OR is associative, commutative and idempotent: the merged words equal a
+ * single-device build of all the keys, bit for bit.  Devices may repeat (the
+ * shards then share a GPU).  Used from one thread at a time. */
+typedef struct lsmb_multi lsmb_multi;
+
+/* devices: ndev HIP ordinals (NULL = 0..ndev-1), 1 <= ndev <= 16.  Enables
+ * peer access between every pair of distinct devices (LSMB_ENODEV if a pair
+ * has no peer path). */
+int lsmb_multi_open(lsmb_multi** out, const int* devices, int ndev);
+void lsmb_multi_close(lsmb_multi* m);
+int lsmb_multi_size(const lsmb_multi* m);
+
+/* Shard g's single-GPU context (its device, stream and scratch), e.g. to place
+ * device buffers or run other entry points on that GPU. */
+lsmb_ctx* lsmb_multi_ctx(lsmb_multi* m, int shard);
+
+/* Device-resident sharded build: shard g's n[g] keys of key_len bytes at
+ * d_keys[g] and its words d_words[g] live on shard g's device.  Every shard
+ * builds into its own words (OR-accumulate), then reduce-scatter + all-gather:
+ * on return every d_words[g] holds the merged filter.  Synchronous. */
+int lsmb_multi_build_fixed_dev(lsmb_multi* m, const void* const* d_keys, const uint64_t* n, uint32_t key_len,
+                               uint32_t num_bits, uint32_t num_hashes, void* const* d_words);
+
+/* lsmb_build_block over G GPUs: the n host-memory keys (fixed-length, or
+ * var-length with offsets) are split into G contiguous shards; each GPU
+ * uploads and builds its shard (G PCIe links in parallel), the partials are
+ * OR-reduce-scattered over xGMI, and each GPU copies its merged word slice
+ * into the block.  Writes exactly BloomFilter::serialize's bytes. */
+int lsmb_multi_build_block(lsmb_multi* m, const uint8_t* data, const uint64_t* offsets, uint32_t key_len,
+                           uint64_t n, uint32_t num_bits, uint32_t num_hashes, uint8_t* block,
+                           uint64_t block_len);
+
+/* Timing of the last multi build, ms: [0] total (slowest shard), [1] build
+ * (slowest shard), [2] merge = [0] - [1]. */
+int lsmb_multi_last_ms(lsmb_multi* m, float* out3);
+
 /* ---- device-resident filter sets (multi-get pre-check) --------------------- */
 /* An lsmb_fset keeps up to 64 SSTable filters resident in device memory, each
  * with its table's key range [min_key, max_key] (SSTable meta,
@@ -222,12 +276,13 @@ int lsmb_fset_probe_dev(lsmb_fset* fs, const void* d_data, const void* d_offsets
 
 /* ---- introspection ------------------------------------------------------- */
 
-/* Name of the build strategy the dispatcher picks for (num_bits, n), e.g.
+/* Name of the device build strategy the dispatcher picks for (num_bits, k, n):
  * "lds", "tiled", "partition", "atomic" (for tests and bench reporting).
+ * Host-memory builds of n <= lsmb_host_max_keys() keys run on the host instead.
  * Measurement switches read at build time: LSMB_FORCE_STRATEGY=atomic,
  * LSMB_SWEEP_PER=1/2 (pass A keys per lane), LSMB_TILED_NO_PREHASH=1,
  * LSMB_H2D_CHUNK_MB, LSMB_WORKSPACE_MB.  The filter bits never depend on them. */
-const char* lsmb_build_strategy(uint32_t num_bits, uint64_t n);
+const char* lsmb_build_strategy(uint32_t num_bits, uint32_t num_hashes, uint64_t n);
 
 /* Timing of the last device build on this context, in milliseconds, per phase
  * (HIP events on the build stream): [0] total, [1] pass A (hash + bin),

@@ -14,8 +14,9 @@
 //   b.build()                       builder.rs:26   b.build()         (one GPU batch)
 // Reference panics (assert!, % by zero) become std::invalid_argument;
 // Err(Error::Corruption(msg)) (src/error.rs:12) becomes lsm::bloom::Corruption.
-// The batched build/probe run on the GPU only: without a gfx950 device they
-// throw (no CPU fallback).
+// The batched build/probe run on the GPU: without a gfx950 device they throw
+// (no CPU fallback), except builds of at most lsmb_host_max_keys() keys, which
+// run the library's own host loop (same bits, no device round trip).
 #pragma once
 
 #include <stdint.h>
@@ -56,9 +57,13 @@ class Context {
     Context(Context&& o) noexcept : c_(o.c_) { o.c_ = nullptr; }
     lsmb_ctx* get() const { return c_; }
 
-    // Process-wide default context, opened on first use.
+    // Default context of the calling thread, opened on first use.  A context
+    // is used by one thread at a time (lsmbloom.h), and the store builds from
+    // more than one thread at once (flush + the background compaction thread,
+    // src/compaction/scheduler.rs:37), so each thread gets its own — the same
+    // choice as the Rust shim's thread_local CTX.
     static Context& shared() {
-        static Context ctx(-1);
+        thread_local Context ctx(-1);
         return ctx;
     }
 
@@ -155,25 +160,30 @@ class BloomFilterBuilder {
     }
     BloomFilter build() {
         if (offsets_.size() > 1) {
-            Context& ctx = ctx_ ? *ctx_ : Context::shared();
-            check(lsmb_build_var(ctx.get(), data_.data(), offsets_.data(), offsets_.size() - 1, filter_.num_bits_,
-                                 filter_.num_hashes_, filter_.bits_.data()));
+            check(lsmb_build_var(ctx_for(offsets_.size() - 1), data_.data(), offsets_.data(), offsets_.size() - 1,
+                                 filter_.num_bits_, filter_.num_hashes_, filter_.bits_.data()));
         }
         return std::move(filter_);
     }
-    // build().serialize() in one GPU call (lsmb_build_block): the bloom block
+    // build().serialize() in one call (lsmb_build_block): the bloom block
     // SSTableBuilder::finish writes (src/sstable/builder.rs:177-179), with the
     // words copied device -> block directly.
     std::vector<uint8_t> build_serialized() {
         std::vector<uint8_t> block(lsmb_serialized_size(filter_.num_bits_));
-        Context& ctx = ctx_ ? *ctx_ : Context::shared();
-        check(lsmb_build_block(ctx.get(), data_.empty() ? nullptr : data_.data(), offsets_.data(), 0,
-                               offsets_.size() - 1, filter_.num_bits_, filter_.num_hashes_, block.data(),
+        check(lsmb_build_block(ctx_for(offsets_.size() - 1), data_.empty() ? nullptr : data_.data(), offsets_.data(),
+                               0, offsets_.size() - 1, filter_.num_bits_, filter_.num_hashes_, block.data(),
                                block.size()));
         return block;
     }
 
    private:
+    // Builds of at most lsmb_host_max_keys() keys (an SST flush at the
+    // reference's default 1 000-key sizing) run the library's host loop and
+    // need no GPU; bigger ones take the GPU context (throws without one).
+    lsmb_ctx* ctx_for(size_t n) {
+        if (n <= lsmb_host_max_keys()) return nullptr;
+        return (ctx_ ? *ctx_ : Context::shared()).get();
+    }
     BloomFilter filter_;
     Context* ctx_;
     std::vector<uint8_t> data_;

@@ -10,19 +10,21 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <string>
+#include <thread>
 #include <vector>
 
-#include "../../include/lsmbloom.h"
-#include "kernels.hpp"
+#include "ctx.hpp"
 
 using namespace lsmb;
 
+namespace lsmb {
+
 namespace {
-
 thread_local std::string g_err;
+}  // namespace
 
-int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 int fail(int code, const char* fmt, ...) {
     char buf[512];
     va_list ap;
@@ -37,44 +39,21 @@ int hip_fail(hipError_t e, const char* what) {
     return fail(LSMB_EHIP, "%s: %s", what, hipGetErrorString(e));
 }
 
-#define HIP_TRY(expr)                                   \
-    do {                                                \
-        hipError_t e_ = (expr);                         \
-        if (e_ != hipSuccess) return hip_fail(e_, #expr); \
-    } while (0)
+const std::string& last_error() { return g_err; }
+void set_last_error(const std::string& s) { g_err = s; }
 
-uint64_t nwords64(uint32_t num_bits) { return ((uint64_t)num_bits + 63) / 64; }
-
-uint32_t rd32le(const uint8_t* p) {
-    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
-}
-
-// Reference arguments that would panic (% by zero in get_position, mod.rs:195).
 int check_filter(uint32_t num_bits, uint32_t k) {
     if (num_bits == 0 && k > 0)
         return fail(LSMB_EINVAL, "num_bits == 0 with num_hashes > 0 (reference panics: %% by zero)");
     return LSMB_OK;
 }
 
-// A grow-only device buffer.
-struct DevBuf {
-    void* p = nullptr;
-    size_t bytes = 0;
-    hipError_t ensure(size_t want) {
-        if (want <= bytes) return hipSuccess;
-        if (p) hipFree(p);
-        p = nullptr;
-        bytes = 0;
-        hipError_t e = hipMalloc(&p, want);
-        if (e == hipSuccess) bytes = want;
-        return e;
-    }
-    void release() {
-        if (p) hipFree(p);
-        p = nullptr;
-        bytes = 0;
-    }
-};
+namespace {
+std::atomic<uint64_t> g_host_max_keys{~0ull};  // ~0: not yet read from the environment
+
+uint32_t rd32le(const uint8_t* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
 
 uint64_t workspace_limit_bytes() {
     const char* s = getenv("LSMB_WORKSPACE_MB");
@@ -82,53 +61,19 @@ uint64_t workspace_limit_bytes() {
     if (mb < 16) mb = 16;
     return mb << 20;
 }
-
 }  // namespace
 
-struct lsmb_ctx {
-    int dev = 0;
-    int num_cus = 256;
-    hipStream_t st = nullptr;
-    BuildTimers tm;
-    DevBuf ws_regions, ws_counts;  // partition workspace
-    DevBuf ws_hashes;              // partition workspace: k_hash records (var-len / odd-length keys)
-    DevBuf err;                    // device error flag of the partition kernels
-    uint32_t* err_host = nullptr;  // pinned mirror read at sync
-    DevBuf keys, offs, words, out; // staging for the host-memory entry points
-    DevBuf filt_words;             // probe: device copies of host filters
-    DevBuf filt_desc;              // probe: ProbeFilter array
-    std::vector<ProbeFilter> hfilt;
-    std::vector<ProbeFilter> desc_uploaded;  // what filt_desc currently holds
-    ProbeFilter* desc_pinned = nullptr;      // pinned staging for descriptor uploads
-    hipEvent_t desc_done = nullptr;          // last kernel that read filt_desc
-    std::vector<uint64_t> offs_tmp;
-    bool timing = true;            // per-build HIP events (lsmb_set_timing)
-    // host-memory builds: two staging slots, H2D on `cst` overlapping the
-    // kernels of the previous chunk on `st` (host_build)
-    hipStream_t cst = nullptr;
-    hipEvent_t ev_copy[2] = {nullptr, nullptr}, ev_built[2] = {nullptr, nullptr};
-    DevBuf kslot[2], oslot[2];
-    uint64_t* offs_pin[2] = {nullptr, nullptr};  // pinned rebased offsets per slot
-    uint64_t offs_pin_cap[2] = {0, 0};
-    uint8_t* pin_small = nullptr;  // pinned staging of small host builds (host_build_small)
-    uint64_t pin_small_cap = 0;
-    bool ran_partition = false;    // a partition build ran since the last error-flag check
-};
+void set_host_max_keys(uint64_t n) { g_host_max_keys.store(n == ~0ull ? n - 1 : n, std::memory_order_relaxed); }
 
-namespace {
-
-struct DevGuard {
-    int prev = -1;
-    explicit DevGuard(int dev) {
-        hipGetDevice(&prev);
-        if (prev != dev) hipSetDevice(dev);
+uint64_t host_max_keys() {
+    uint64_t v = g_host_max_keys.load(std::memory_order_relaxed);
+    if (v == ~0ull) {
+        const char* s = getenv("LSMB_HOST_MAX_KEYS");
+        v = s ? strtoull(s, nullptr, 10) : kDefaultHostMaxKeys;
+        g_host_max_keys.store(v, std::memory_order_relaxed);
     }
-    ~DevGuard() {
-        int cur = -1;
-        hipGetDevice(&cur);
-        if (prev >= 0 && cur != prev) hipSetDevice(prev);
-    }
-};
+    return v;
+}
 
 hipStream_t pick_stream(lsmb_ctx* c, void* stream) {
     return stream ? reinterpret_cast<hipStream_t>(stream) : c->st;
@@ -149,16 +94,23 @@ int check_device_error(lsmb_ctx* c) {
     // round trip) after builds that ran none.
     if (!c->ran_partition) return LSMB_OK;
     c->ran_partition = false;
-    HIP_TRY(hipMemcpy(c->err_host, c->err.p, 32, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpyAsync(c->err_host, c->err.p, 32, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
     if (*c->err_host) {
         uint32_t e[8];
         memcpy(e, c->err_host, 32);
-        HIP_TRY(hipMemset(c->err.p, 0, 32));
+        HIP_TRY(hipMemsetAsync(c->err.p, 0, 32, c->st));
+        HIP_TRY(hipStreamSynchronize(c->st));
         return fail(LSMB_EHIP, "partition build: bounded wait timed out (internal error, code %u, diag %u %u %u %u)",
                     e[0], e[1], e[2], e[3], e[4]);
     }
     return LSMB_OK;
 }
+
+namespace {
+int build_dev_ws(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k, uint32_t* dw, hipStream_t st,
+                 BuildStrategy s);
+}  // namespace
 
 // Device build of one batch, chunked so the partition workspace stays bounded.
 int build_dev(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k, uint32_t* dw,
@@ -170,6 +122,21 @@ int build_dev(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k
         if ((s == BuildStrategy::Partition || s == BuildStrategy::Tiled) && !strcmp(f, "atomic")) s = BuildStrategy::Atomic;
     c->tm.valid = false;
     if (s == BuildStrategy::None) return LSMB_OK;
+    if (s != BuildStrategy::Tiled && s != BuildStrategy::Partition)
+        return build_dev_ws(c, kb_all, num_bits, k, dw, st, s);
+    // Tiled and partition builds use the context's shared workspace: a build
+    // issued on a different stream than the last one waits for it (two
+    // streams' builds would otherwise overwrite each other's regions).
+    if (c->ws_stream) HIP_TRY(hipStreamWaitEvent(st, c->ws_done, 0));
+    const int rc = build_dev_ws(c, kb_all, num_bits, k, dw, st, s);
+    HIP_TRY(hipEventRecord(c->ws_done, st));
+    c->ws_stream = st;
+    return rc;
+}
+
+namespace {
+int build_dev_ws(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k, uint32_t* dw, hipStream_t st,
+                 BuildStrategy s) {
     if (s == BuildStrategy::Tiled) {
         const TiledPlan tp = plan_tiled(num_bits, kb_all.n, c->num_cus);
         HIP_TRY(c->ws_regions.ensure(tp.scratch_bytes));
@@ -218,6 +185,7 @@ int build_dev(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k
     }
     return LSMB_OK;
 }
+}  // namespace
 
 // Host single-key walks (the same arithmetic the kernels run).
 template <class W, class F>
@@ -314,20 +282,8 @@ int host_build_small(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, 
     return check_device_error(c);
 }
 
-int host_build(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
-               uint32_t num_bits, uint32_t k, const uint64_t* words_in, uint8_t* words_out) {
-    const uint64_t nw = nwords64(num_bits);
-    {
-        const uint64_t kb = offsets ? offsets[n] - offsets[0] : n * (uint64_t)key_len;
-        if (kb + (offsets ? (n + 1) * 8 : 0) + nw * 8 <= kSmallHostBuild)
-            return host_build_small(c, data, offsets, key_len, n, num_bits, k, words_in, words_out);
-    }
-    HIP_TRY(c->words.ensure(nw * 8));
-    uint32_t* dw = (uint32_t*)c->words.p;
-    if (words_in)
-        HIP_TRY(hipMemcpyAsync(dw, words_in, nw * 8, hipMemcpyHostToDevice, c->st));
-    else
-        HIP_TRY(hipMemsetAsync(dw, 0, nw * 8, c->st));
+int host_build_dev(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
+                   uint32_t num_bits, uint32_t k, uint32_t* dw) {
     if (!offsets && key_len == 0) {
         // every key is the empty key: one insert covers them all
         HIP_TRY(c->kslot[0].ensure(16));
@@ -377,14 +333,58 @@ int host_build(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, uint32
         HIP_TRY(hipEventRecord(c->ev_built[s], c->st));
         f = e;
     }
+    return LSMB_OK;
+}
+
+int host_build(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
+               uint32_t num_bits, uint32_t k, const uint64_t* words_in, uint8_t* words_out) {
+    const uint64_t nw = nwords64(num_bits);
+    {
+        const uint64_t kb = offsets ? offsets[n] - offsets[0] : n * (uint64_t)key_len;
+        if (kb + (offsets ? (n + 1) * 8 : 0) + nw * 8 <= kSmallHostBuild)
+            return host_build_small(c, data, offsets, key_len, n, num_bits, k, words_in, words_out);
+    }
+    HIP_TRY(c->words.ensure(nw * 8));
+    uint32_t* dw = (uint32_t*)c->words.p;
+    if (words_in)
+        HIP_TRY(hipMemcpyAsync(dw, words_in, nw * 8, hipMemcpyHostToDevice, c->st));
+    else
+        HIP_TRY(hipMemsetAsync(dw, 0, nw * 8, c->st));
+    if (int rc = host_build_dev(c, data, offsets, key_len, n, num_bits, k, dw)) return rc;
     HIP_TRY(hipMemcpyAsync(words_out, dw, nw * 8, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(hipStreamSynchronize(c->st));
     return check_device_error(c);
 }
 
-}  // namespace
+// The library's own host build: BloomFilter::insert per key
+// (src/bloom/mod.rs:70-78) with the same xxh3 / exact-modulo code the kernels
+// run, compiled for the host.  Used below host_max_keys(), where a device round
+// trip (H2D, launch, D2H, sync: ~40 us) costs more than the whole loop.
+template <class W>
+static void host_insert_batch_w(const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
+                                uint32_t num_bits, uint32_t k, uint64_t* words) {
+    const Mod32 md = Mod32::make(num_bits);
+    for (uint64_t i = 0; i < n; i++) {
+        const uint8_t* key = offsets ? data + offsets[i] : data + i * (uint64_t)key_len;
+        const uint64_t len = offsets ? offsets[i + 1] - offsets[i] : key_len;
+        const H128 h = xxh3_128(key, len);
+        W w(md, h.lo, h.hi);
+        for (uint32_t j = 0; j < k; j++) {
+            const uint32_t p = w.pos();
+            words[p >> 6] |= 1ull << (p & 63);
+            w.next(md);
+        }
+    }
+}
 
-namespace lsmb {
+void host_insert_batch(const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
+                       uint32_t num_bits, uint32_t k, uint64_t* words) {
+    if (k == 0 || n == 0) return;
+    if (fits_walk32(num_bits))
+        host_insert_batch_w<Walk32>(data, offsets, key_len, n, num_bits, k, words);
+    else
+        host_insert_batch_w<Walk64>(data, offsets, key_len, n, num_bits, k, words);
+}
 
 bool bloom_params(uint64_t n, double fpr, uint32_t* num_bits, uint32_t* num_hashes) {
     if (n == 0 || !(fpr > 0.0 && fpr < 1.0)) return false;
@@ -408,7 +408,7 @@ bool bloom_params(uint64_t n, double fpr, uint32_t* num_bits, uint32_t* num_hash
 extern "C" {
 
 int lsmb_abi_version(void) { return LSMB_ABI_VERSION; }
-const char* lsmb_last_error(void) { return g_err.c_str(); }
+const char* lsmb_last_error(void) { return last_error().c_str(); }
 
 int lsmb_params(uint64_t n, double fpr, uint32_t* num_bits, uint32_t* num_hashes) {
     if (!num_bits || !num_hashes) return fail(LSMB_EINVAL, "null output pointer");
@@ -505,8 +505,11 @@ int lsmb_open(lsmb_ctx** out, int device) {
     c->dev = device;
     c->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     DevGuard g(device);
-    if (hipStreamCreateWithFlags(&c->st, hipStreamDefault) != hipSuccess ||
+    // Non-blocking streams: no implicit ordering with the legacy null stream,
+    // so one context's work never waits for another's (flush + compaction).
+    if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->desc_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ws_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreate(&c->tm.t0) != hipSuccess || hipEventCreate(&c->tm.t1) != hipSuccess ||
         hipEventCreate(&c->tm.t2) != hipSuccess ||
         hipStreamCreateWithFlags(&c->cst, hipStreamNonBlocking) != hipSuccess ||
@@ -547,6 +550,7 @@ void lsmb_close(lsmb_ctx* c) {
         hipEventDestroy(c->tm.t1);
         hipEventDestroy(c->tm.t2);
         hipEventDestroy(c->desc_done);
+        if (c->ws_done) hipEventDestroy(c->ws_done);
         if (c->desc_pinned) hipHostFree(c->desc_pinned);
         hipStreamDestroy(c->st);
     }
@@ -586,31 +590,48 @@ int lsmb_build_var_dev(lsmb_ctx* c, const void* d_data, const void* d_offsets, u
     return build_dev(c, kb, num_bits, k, (uint32_t*)d_words, pick_stream(c, stream));
 }
 
+// Builds of n <= host_max_keys() keys run the library's host loop (no device
+// round trip, ctx may be NULL); bigger ones need a device context.
+static int need_ctx(lsmb_ctx* c, uint64_t n) {
+    if (!c)
+        return fail(LSMB_EINVAL, "null ctx: builds of more than %llu keys run on the GPU (lsmb_host_max_keys)",
+                    (unsigned long long)host_max_keys());
+    (void)n;
+    return LSMB_OK;
+}
+
 int lsmb_build_fixed(lsmb_ctx* c, const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t num_bits,
                      uint32_t k, uint64_t* words) {
-    if (!c) return fail(LSMB_EINVAL, "null ctx");
     if (int rc = check_filter(num_bits, k)) return rc;
     if (n == 0 || k == 0) return LSMB_OK;
     if (!keys && key_len) return fail(LSMB_EINVAL, "null keys");
     if (!words) return fail(LSMB_EINVAL, "null words");
+    if (n <= host_max_keys()) {
+        host_insert_batch(keys, nullptr, key_len, key_len ? n : 1, num_bits, k, words);
+        return LSMB_OK;
+    }
+    if (int rc = need_ctx(c, n)) return rc;
     DevGuard g(c->dev);
     return host_build(c, keys, nullptr, key_len, n, num_bits, k, words, (uint8_t*)words);
 }
 
 int lsmb_build_var(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, uint64_t n,
                    uint32_t num_bits, uint32_t k, uint64_t* words) {
-    if (!c) return fail(LSMB_EINVAL, "null ctx");
     if (int rc = check_filter(num_bits, k)) return rc;
     if (n == 0 || k == 0) return LSMB_OK;
     if (!offsets || !words) return fail(LSMB_EINVAL, "null pointer");
     if (int rc = check_offsets(offsets, n)) return rc;
+    if (n <= host_max_keys()) {
+        host_insert_batch(data, offsets, 0, n, num_bits, k, words);
+        return LSMB_OK;
+    }
+    if (int rc = need_ctx(c, n)) return rc;
     DevGuard g(c->dev);
     return host_build(c, data, offsets, 0, n, num_bits, k, words, (uint8_t*)words);
 }
 
 int lsmb_build_block(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
                      uint32_t num_bits, uint32_t k, uint8_t* block, uint64_t block_len) {
-    if (!c) return fail(LSMB_EINVAL, "null ctx");
     if (int rc = check_filter(num_bits, k)) return rc;
     const uint64_t nw = nwords64(num_bits);
     const uint64_t size = 12 + 8 * nw;
@@ -630,9 +651,22 @@ int lsmb_build_block(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, 
         memset(block + 12, 0, nw * 8);
         return LSMB_OK;
     }
+    if (n <= host_max_keys()) {
+        // the block body is not 8-byte aligned (12-B header): build into an
+        // aligned word array, then copy
+        std::vector<uint64_t> w(nw, 0);
+        host_insert_batch(data, offsets, key_len, (!offsets && key_len == 0) ? 1 : n, num_bits, k, w.data());
+        memcpy(block + 12, w.data(), nw * 8);
+        return LSMB_OK;
+    }
+    if (int rc = need_ctx(c, n)) return rc;
     DevGuard g(c->dev);
     return host_build(c, data, offsets, key_len, n, num_bits, k, nullptr, block + 12);
 }
+
+uint64_t lsmb_host_max_keys(void) { return host_max_keys(); }
+
+void lsmb_set_host_max_keys(uint64_t n) { set_host_max_keys(n); }
 
 // Copies a host key batch into the context's staging buffers (ctx stream).
 static int stage_host_keys(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
@@ -767,8 +801,8 @@ int lsmb_gen_key16_dev(lsmb_ctx* c, uint64_t seed, uint64_t first, uint64_t n, v
     return LSMB_OK;
 }
 
-const char* lsmb_build_strategy(uint32_t num_bits, uint64_t n) {
-    return strategy_name(pick_build_strategy(num_bits, 7, n));
+const char* lsmb_build_strategy(uint32_t num_bits, uint32_t k, uint64_t n) {
+    return strategy_name(pick_build_strategy(num_bits, k, n));
 }
 
 int lsmb_set_timing(lsmb_ctx* c, int enable) {
@@ -806,9 +840,34 @@ struct lsmb_fset {
     uint32_t ndesc = 0;
     uint32_t shared_nb = 0, shared_k = 0;  // (num_bits, k) of every live slot, or 0 when they differ
     bool dirty = true;
+    // Uploads go through the set's own non-blocking stream; before a buffer a
+    // probe may still read is rewritten, the host waits for the events
+    // recorded after this set's probes (one per stream used) — never for the
+    // whole device, so another context's builds keep running.
+    hipStream_t ust = nullptr;
+    std::vector<std::pair<hipStream_t, hipEvent_t>> probe_ev;
 };
 
 namespace {
+
+int fset_wait_probes(lsmb_fset* fs) {
+    for (auto& pe : fs->probe_ev) HIP_TRY(hipEventSynchronize(pe.second));
+    return LSMB_OK;
+}
+
+// After a probe on stream st: remember it so later rewrites wait for it.
+int fset_note_probe(lsmb_fset* fs, hipStream_t st) {
+    for (auto& pe : fs->probe_ev)
+        if (pe.first == st) {
+            HIP_TRY(hipEventRecord(pe.second, st));
+            return LSMB_OK;
+        }
+    hipEvent_t ev;
+    HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    fs->probe_ev.push_back({st, ev});
+    HIP_TRY(hipEventRecord(ev, st));
+    return LSMB_OK;
+}
 
 // Rebuilds the device descriptors after an add/remove (rare; probes re-use them).
 int fset_refresh(lsmb_fset* fs) {
@@ -823,9 +882,13 @@ int fset_refresh(lsmb_fset* fs) {
         blob.insert(blob.end(), S.lo.begin(), S.lo.end());
         blob.insert(blob.end(), S.hi.begin(), S.hi.end());
     }
-    HIP_TRY(hipDeviceSynchronize());  // no probe may still read the old descriptors
-    HIP_TRY(fs->ranges.ensure(std::max<size_t>(blob.size(), 16)));
-    if (!blob.empty()) HIP_TRY(hipMemcpy(fs->ranges.p, blob.data(), blob.size(), hipMemcpyHostToDevice));
+    if (int rc = fset_wait_probes(fs)) return rc;  // no probe may still read the old descriptors
+    // grow geometrically from 4 KiB: a re-allocation frees the old buffer, and
+    // hipFree waits for the whole device
+    size_t want = 4096;
+    while (want < blob.size()) want *= 2;
+    HIP_TRY(fs->ranges.ensure(want));
+    if (!blob.empty()) HIP_TRY(hipMemcpyAsync(fs->ranges.p, blob.data(), blob.size(), hipMemcpyHostToDevice, fs->ust));
     const uint8_t* rb = (const uint8_t*)fs->ranges.p;
     uint32_t j = 0;
     for (uint32_t s = 0; s < 64; s++) {
@@ -847,7 +910,9 @@ int fset_refresh(lsmb_fset* fs) {
         j++;
     }
     HIP_TRY(fs->desc.ensure(sizeof(RangedFilter) * 64));
-    if (!d.empty()) HIP_TRY(hipMemcpy(fs->desc.p, d.data(), sizeof(RangedFilter) * d.size(), hipMemcpyHostToDevice));
+    if (!d.empty())
+        HIP_TRY(hipMemcpyAsync(fs->desc.p, d.data(), sizeof(RangedFilter) * d.size(), hipMemcpyHostToDevice, fs->ust));
+    HIP_TRY(hipStreamSynchronize(fs->ust));  // blob and d are host temporaries
     fs->ndesc = (uint32_t)d.size();
     fs->shared_nb = d.empty() ? 0 : d[0].f.num_bits;
     fs->shared_k = d.empty() ? 0 : d[0].f.k;
@@ -868,9 +933,12 @@ int fset_add_common(lsmb_fset* fs, const uint8_t* words_le, uint32_t num_bits, u
     DevGuard g(fs->c->dev);
     auto& S = fs->slot[s];
     const uint64_t nw = nwords64(num_bits);
-    HIP_TRY(hipDeviceSynchronize());  // the slot's old buffer may still be read by a probe
+    if (int rc = fset_wait_probes(fs)) return rc;  // the slot's old buffer may still be read by a probe
     HIP_TRY(S.words.ensure(std::max<uint64_t>(nw, 2) * 8));
-    if (nw) HIP_TRY(hipMemcpy(S.words.p, words_le, nw * 8, hipMemcpyHostToDevice));
+    if (nw) {
+        HIP_TRY(hipMemcpyAsync(S.words.p, words_le, nw * 8, hipMemcpyHostToDevice, fs->ust));
+        HIP_TRY(hipStreamSynchronize(fs->ust));
+    }
     S.num_bits = num_bits;
     S.k = k;
     S.lo.assign(min_key, min_key + min_len);
@@ -884,8 +952,15 @@ int fset_add_common(lsmb_fset* fs, const uint8_t* words_le, uint32_t num_bits, u
 
 int lsmb_fset_open(lsmb_ctx* c, lsmb_fset** out) {
     if (!c || !out) return fail(LSMB_EINVAL, "null argument");
-    *out = new lsmb_fset;
-    (*out)->c = c;
+    *out = nullptr;
+    DevGuard g(c->dev);
+    lsmb_fset* fs = new lsmb_fset;
+    fs->c = c;
+    if (hipStreamCreateWithFlags(&fs->ust, hipStreamNonBlocking) != hipSuccess) {
+        delete fs;
+        return fail(LSMB_EHIP, "filter set: stream creation failed");
+    }
+    *out = fs;
     return LSMB_OK;
 }
 
@@ -893,7 +968,9 @@ void lsmb_fset_close(lsmb_fset* fs) {
     if (!fs) return;
     {
         DevGuard g(fs->c->dev);
-        hipDeviceSynchronize();
+        fset_wait_probes(fs);
+        for (auto& pe : fs->probe_ev) hipEventDestroy(pe.second);
+        if (fs->ust) hipStreamSynchronize(fs->ust), hipStreamDestroy(fs->ust);
         for (auto& S : fs->slot) S.words.release();
         fs->ranges.release();
         fs->desc.release();
@@ -946,7 +1023,7 @@ int lsmb_fset_probe_dev(lsmb_fset* fs, const void* d_data, const void* d_offsets
     }
     KeyBatch kb{(const uint8_t*)d_data, (const uint64_t*)d_offsets, key_len, n};
     HIP_TRY(launch_fset_probe(kb, (const RangedFilter*)fs->desc.p, fs->ndesc, fs->shared_nb, fs->shared_k, (uint64_t*)d_out, fs->c->num_cus, st));
-    return LSMB_OK;
+    return fset_note_probe(fs, st);
 }
 
 int lsmb_fset_probe(lsmb_fset* fs, const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
@@ -966,6 +1043,7 @@ int lsmb_fset_probe(lsmb_fset* fs, const uint8_t* data, const uint64_t* offsets,
         return LSMB_OK;
     }
     HIP_TRY(launch_fset_probe(kb, (const RangedFilter*)fs->desc.p, fs->ndesc, fs->shared_nb, fs->shared_k, (uint64_t*)c->out.p, c->num_cus, c->st));
+    if (int rc = fset_note_probe(fs, c->st)) return rc;
     HIP_TRY(hipMemcpyAsync(out_mask, c->out.p, n * 8, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(hipStreamSynchronize(c->st));
     return LSMB_OK;

@@ -1,0 +1,130 @@
+// ctx.hpp — the per-GPU context behind lsmb_ctx and the host plumbing shared by
+// capi.hip (single GPU) and multi.hip (one process, several GPUs).  Internal.
+#pragma once
+
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/lsmbloom.h"
+#include "kernels.hpp"
+
+namespace lsmb {
+
+// A grow-only device buffer.
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t want) {
+        if (want <= bytes) return hipSuccess;
+        if (p) hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) bytes = want;
+        return e;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+};
+
+struct DevGuard {
+    int prev = -1;
+    explicit DevGuard(int dev) {
+        hipGetDevice(&prev);
+        if (prev != dev) hipSetDevice(dev);
+    }
+    ~DevGuard() {
+        int cur = -1;
+        hipGetDevice(&cur);
+        if (prev >= 0 && cur != prev) hipSetDevice(prev);
+    }
+};
+
+// Thread-local error message (lsmb_last_error) and the error returns.
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int hip_fail(hipError_t e, const char* what);
+const std::string& last_error();
+void set_last_error(const std::string& s);
+
+#define HIP_TRY(expr)                                           \
+    do {                                                        \
+        hipError_t e_ = (expr);                                 \
+        if (e_ != hipSuccess) return ::lsmb::hip_fail(e_, #expr); \
+    } while (0)
+
+inline uint64_t nwords64(uint32_t num_bits) { return ((uint64_t)num_bits + 63) / 64; }
+
+// Reference arguments that would panic (% by zero in get_position, mod.rs:195).
+int check_filter(uint32_t num_bits, uint32_t k);
+
+// Builds of at most this many keys run the library's host loop (the
+// reference's own per-key insert, src/bloom/mod.rs:70-78) instead of a device
+// round trip; see lsmb_host_max_keys().
+uint64_t host_max_keys();
+void set_host_max_keys(uint64_t n);
+constexpr uint64_t kDefaultHostMaxKeys = 2048;  // SST-sized flush latency
+
+}  // namespace lsmb
+
+struct lsmb_ctx {
+    int dev = 0;
+    int num_cus = 256;
+    hipStream_t st = nullptr;
+    lsmb::BuildTimers tm;
+    lsmb::DevBuf ws_regions, ws_counts;  // partition / tiled workspace
+    lsmb::DevBuf ws_hashes;              // k_hash records (var-len / odd-length keys)
+    lsmb::DevBuf err;                    // device error flag of the partition kernels
+    uint32_t* err_host = nullptr;        // pinned mirror read at sync
+    // The workspace above is shared by every build on this context, whatever
+    // stream it is issued on: ws_done marks the last build that used it, and a
+    // build on another stream waits for it first (build_dev).
+    hipEvent_t ws_done = nullptr;
+    hipStream_t ws_stream = nullptr;     // stream of the last workspace user (nullptr: none yet)
+    lsmb::DevBuf keys, offs, words, out; // staging for the host-memory entry points
+    lsmb::DevBuf filt_words;             // probe: device copies of host filters
+    lsmb::DevBuf filt_desc;              // probe: ProbeFilter array
+    std::vector<lsmb::ProbeFilter> hfilt;
+    std::vector<lsmb::ProbeFilter> desc_uploaded;  // what filt_desc currently holds
+    lsmb::ProbeFilter* desc_pinned = nullptr;      // pinned staging for descriptor uploads
+    hipEvent_t desc_done = nullptr;                // last kernel that read filt_desc
+    std::vector<uint64_t> offs_tmp;
+    bool timing = true;                  // per-build HIP events (lsmb_set_timing)
+    // host-memory builds: two staging slots, H2D on `cst` overlapping the
+    // kernels of the previous chunk on `st` (host_build_dev)
+    hipStream_t cst = nullptr;
+    hipEvent_t ev_copy[2] = {nullptr, nullptr}, ev_built[2] = {nullptr, nullptr};
+    lsmb::DevBuf kslot[2], oslot[2];
+    uint64_t* offs_pin[2] = {nullptr, nullptr};  // pinned rebased offsets per slot
+    uint64_t offs_pin_cap[2] = {0, 0};
+    uint8_t* pin_small = nullptr;  // pinned staging of small host builds (host_build_small)
+    uint64_t pin_small_cap = 0;
+    bool ran_partition = false;    // a partition build ran since the last error-flag check
+};
+
+namespace lsmb {
+
+// Device build of one batch on `st` into d_words (OR-accumulate), chunked so
+// the partition workspace stays bounded.  Asynchronous.
+int build_dev(lsmb_ctx* c, const KeyBatch& kb, uint32_t num_bits, uint32_t k, uint32_t* d_words, hipStream_t st);
+
+// Keys in host memory -> OR-accumulated into the device words dw (already
+// zeroed or loaded by the caller) on c->st: chunked H2D through the two
+// staging slots, overlapped with the build.  Returns once everything is
+// enqueued; the caller synchronises c->st.
+int host_build_dev(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
+                   uint32_t num_bits, uint32_t k, uint32_t* dw);
+
+// Host build (the library's native per-key loop) into words (OR-accumulate).
+void host_insert_batch(const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
+                       uint32_t num_bits, uint32_t k, uint64_t* words);
+
+// Reads (and clears) the kernels' device error flag.  Requires the work that
+// could set it to have completed.
+int check_device_error(lsmb_ctx* c);
+
+}  // namespace lsmb

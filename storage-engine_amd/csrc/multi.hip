@@ -1,0 +1,371 @@
+// multi.hip — one process, several GPUs: a sharded build merged over xGMI.
+//
+// The store flushes and compacts from one process (src/db/mod.rs:377-383,
+// src/compaction/scheduler.rs:150-158, both through SSTableBuilder::add,
+// src/sstable/builder.rs:93).  When one run's key set is large, lsmb_multi
+// splits it into G contiguous shards, builds a full-size partial filter per
+// shard on its own GPU, and merges the partials with a bitwise-OR
+// reduce-scatter done by peer loads: shard g's GPU reads word-slice g of every
+// partial straight out of the other GPUs' HBM over xGMI and ORs it (no staging
+// copy, every peer link busy at once).  OR is associative, commutative and
+// idempotent, so the merged filter is bit-identical to a single-GPU build of
+// the whole run.  RCCL has no bitwise-OR reduction (rccl.h ncclRedOp_t), and
+// inside one process peer loads need no communicator at all.
+//
+//   device-resident (lsmb_multi_build_fixed_dev): + all-gather of the merged
+//     slices, so every GPU ends up holding the whole filter;
+//   host keys -> serialized block (lsmb_multi_build_block): each GPU uploads
+//     its own shard (G PCIe links in parallel) and copies only its merged
+//     slice into the block (again G links in parallel); no all-gather.
+//
+// Shards may name the same device more than once (tests on a one-GPU box run
+// G = 2..4 shards on device 0: the same kernels and the same merge, with the
+// "peer" reads served locally).
+#include <stdarg.h>
+#include <string.h>
+
+#include <algorithm>
+#include <thread>
+#include <vector>
+
+#include "ctx.hpp"
+
+using namespace lsmb;
+
+namespace {
+
+constexpr int kMaxShards = 16;
+
+struct OrSources {
+    const void* p[kMaxShards];
+    uint32_t n;
+};
+
+// dst[i] = OR over j of src_j[i], i < count (elements of V).  dst may be one
+// of the sources (the owner's own partial): each element is read by every
+// source load before its one store, by the same thread.
+template <class V>
+__global__ __launch_bounds__(256) void k_or_gather(V* __restrict__ dst, OrSources src, uint64_t count) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
+        V v = static_cast<const V*>(src.p[0])[i];
+        for (uint32_t j = 1; j < src.n; j++) {
+            const V w = static_cast<const V*>(src.p[j])[i];
+            if constexpr (sizeof(V) == 16) {
+                v.x |= w.x, v.y |= w.y, v.z |= w.z, v.w |= w.w;
+            } else {
+                v |= w;
+            }
+        }
+        dst[i] = v;
+    }
+}
+
+hipError_t launch_or_gather(uint64_t* dst, const OrSources& s, uint64_t nwords, int num_cus, hipStream_t st) {
+    if (nwords == 0) return hipSuccess;
+    bool a16 = ((uintptr_t)dst & 15) == 0 && (nwords & 1) == 0;
+    for (uint32_t j = 0; j < s.n; j++) a16 = a16 && ((uintptr_t)s.p[j] & 15) == 0;
+    const uint64_t count = a16 ? nwords / 2 : nwords;
+    uint64_t g = (count + 255) / 256;
+    g = std::min<uint64_t>(g, (uint64_t)num_cus * 8);
+    if (g < 1) g = 1;
+    if (a16)
+        k_or_gather<uint4><<<dim3((uint32_t)g), dim3(256), 0, st>>>((uint4*)dst, s, count);
+    else
+        k_or_gather<uint64_t><<<dim3((uint32_t)g), dim3(256), 0, st>>>(dst, s, count);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+struct lsmb_multi {
+    std::vector<lsmb_ctx*> ctx;  // one per shard
+    std::vector<hipEvent_t> ev_built, ev_merged;  // per shard, recorded on the shard's stream
+    std::vector<hipEvent_t> t0, t1, t2;           // timing per shard: start, built, merged
+    std::vector<DevBuf> words;                    // per-shard device words (host-key builds)
+    bool timed = false;
+};
+
+namespace {
+
+int shards(const lsmb_multi* m) { return (int)m->ctx.size(); }
+
+// Word-slice g of an nw-word filter: [g*per, min((g+1)*per, nw)), per even so
+// every slice starts 16-B aligned.
+uint64_t slice_words(uint64_t nw, int G) {
+    uint64_t per = (nw + G - 1) / G;
+    return (per + 1) & ~1ull;
+}
+
+void slice_of(uint64_t nw, int G, int g, uint64_t* lo, uint64_t* hi) {
+    const uint64_t per = slice_words(nw, G);
+    *lo = std::min<uint64_t>(nw, (uint64_t)g * per);
+    *hi = std::min<uint64_t>(nw, (uint64_t)(g + 1) * per);
+}
+
+// Runs f(g) for every shard on its own host thread (each sets its device);
+// returns the first failure with its message.
+template <class F>
+int for_shards(lsmb_multi* m, F&& f) {
+    const int G = shards(m);
+    std::vector<int> rc(G, LSMB_OK);
+    std::vector<std::string> msg(G);
+    std::vector<std::thread> th;
+    for (int g = 0; g < G; g++)
+        th.emplace_back([&, g]() {
+            DevGuard dg(m->ctx[g]->dev);
+            rc[g] = f(g);
+            if (rc[g]) msg[g] = last_error();
+        });
+    for (auto& t : th) t.join();
+    for (int g = 0; g < G; g++)
+        if (rc[g]) {
+            set_last_error("shard " + std::to_string(g) + ": " + msg[g]);
+            return rc[g];
+        }
+    return LSMB_OK;
+}
+
+// Reduce-scatter: after every shard's build (ev_built), shard g ORs slice g of
+// all partials into its own partial.  `part[j]` = shard j's words (device of j).
+int merge_reduce_scatter(lsmb_multi* m, uint64_t* const* part, uint64_t nw) {
+    const int G = shards(m);
+    for (int g = 0; g < G; g++) {
+        lsmb_ctx* c = m->ctx[g];
+        DevGuard dg(c->dev);
+        for (int j = 0; j < G; j++)
+            if (j != g) HIP_TRY(hipStreamWaitEvent(c->st, m->ev_built[j], 0));
+        uint64_t lo, hi;
+        slice_of(nw, G, g, &lo, &hi);
+        OrSources s;
+        s.n = (uint32_t)G;
+        for (int j = 0; j < G; j++) s.p[j] = part[j] + lo;
+        HIP_TRY(launch_or_gather(part[g] + lo, s, hi - lo, c->num_cus, c->st));
+        HIP_TRY(hipEventRecord(m->ev_merged[g], c->st));
+    }
+    return LSMB_OK;
+}
+
+// All-gather: shard g copies every other shard's merged slice into its words.
+int merge_all_gather(lsmb_multi* m, uint64_t* const* part, uint64_t nw) {
+    const int G = shards(m);
+    for (int g = 0; g < G; g++) {
+        lsmb_ctx* c = m->ctx[g];
+        DevGuard dg(c->dev);
+        for (int j = 0; j < G; j++) {
+            if (j == g) continue;
+            HIP_TRY(hipStreamWaitEvent(c->st, m->ev_merged[j], 0));
+            uint64_t lo, hi;
+            slice_of(nw, G, j, &lo, &hi);
+            if (hi == lo) continue;
+            const int dj = m->ctx[j]->dev;
+            if (dj == c->dev)
+                HIP_TRY(hipMemcpyAsync(part[g] + lo, part[j] + lo, (hi - lo) * 8, hipMemcpyDeviceToDevice, c->st));
+            else
+                HIP_TRY(hipMemcpyPeerAsync(part[g] + lo, c->dev, part[j] + lo, dj, (hi - lo) * 8, c->st));
+        }
+    }
+    return LSMB_OK;
+}
+
+int sync_all(lsmb_multi* m) {
+    for (lsmb_ctx* c : m->ctx) {
+        DevGuard dg(c->dev);
+        HIP_TRY(hipStreamSynchronize(c->st));
+        if (int rc = check_device_error(c)) return rc;
+    }
+    return LSMB_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lsmb_multi_open(lsmb_multi** out, const int* devices, int ndev) {
+    if (!out) return fail(LSMB_EINVAL, "null lsmb_multi pointer");
+    *out = nullptr;
+    if (ndev < 1 || ndev > kMaxShards) return fail(LSMB_EINVAL, "ndev must be in [1, %d]", kMaxShards);
+    lsmb_multi* m = new lsmb_multi;
+    for (int g = 0; g < ndev; g++) {
+        lsmb_ctx* c = nullptr;
+        const int d = devices ? devices[g] : g;
+        if (int rc = lsmb_open(&c, d)) {
+            lsmb_multi_close(m);
+            return rc;
+        }
+        m->ctx.push_back(c);
+    }
+    // Peer access between every pair of distinct devices: the merge kernel
+    // reads the other GPUs' partials in place.
+    for (int g = 0; g < ndev; g++) {
+        DevGuard dg(m->ctx[g]->dev);
+        for (int j = 0; j < ndev; j++) {
+            const int a = m->ctx[g]->dev, b = m->ctx[j]->dev;
+            if (a == b) continue;
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, a, b) != hipSuccess || !can) {
+                lsmb_multi_close(m);
+                return fail(LSMB_ENODEV, "device %d cannot access device %d's memory (no xGMI peer path)", a, b);
+            }
+            hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+            if (e == hipErrorPeerAccessAlreadyEnabled) {
+                (void)hipGetLastError();
+            } else if (e != hipSuccess) {
+                lsmb_multi_close(m);
+                return hip_fail(e, "hipDeviceEnablePeerAccess");
+            }
+        }
+        m->ev_built.push_back(nullptr);
+        m->ev_merged.push_back(nullptr);
+        m->t0.push_back(nullptr);
+        m->t1.push_back(nullptr);
+        m->t2.push_back(nullptr);
+        if (hipEventCreateWithFlags(&m->ev_built[g], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&m->ev_merged[g], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreate(&m->t0[g]) != hipSuccess || hipEventCreate(&m->t1[g]) != hipSuccess ||
+            hipEventCreate(&m->t2[g]) != hipSuccess) {
+            lsmb_multi_close(m);
+            return fail(LSMB_EHIP, "event creation failed on device %d", m->ctx[g]->dev);
+        }
+    }
+    m->words.resize(ndev);
+    *out = m;
+    return LSMB_OK;
+}
+
+void lsmb_multi_close(lsmb_multi* m) {
+    if (!m) return;
+    for (size_t g = 0; g < m->ctx.size(); g++) {
+        DevGuard dg(m->ctx[g]->dev);
+        hipStreamSynchronize(m->ctx[g]->st);
+        for (auto* v : {&m->ev_built, &m->ev_merged, &m->t0, &m->t1, &m->t2})
+            if (g < v->size() && (*v)[g]) hipEventDestroy((*v)[g]);
+        if (g < m->words.size()) m->words[g].release();
+    }
+    for (lsmb_ctx* c : m->ctx) lsmb_close(c);
+    delete m;
+}
+
+int lsmb_multi_size(const lsmb_multi* m) { return m ? shards(m) : 0; }
+
+lsmb_ctx* lsmb_multi_ctx(lsmb_multi* m, int shard) {
+    if (!m || shard < 0 || shard >= shards(m)) return nullptr;
+    return m->ctx[shard];
+}
+
+int lsmb_multi_build_fixed_dev(lsmb_multi* m, const void* const* d_keys, const uint64_t* n, uint32_t key_len,
+                               uint32_t num_bits, uint32_t k, void* const* d_words) {
+    if (!m || !d_keys || !n || !d_words) return fail(LSMB_EINVAL, "null argument");
+    if (int rc = check_filter(num_bits, k)) return rc;
+    const int G = shards(m);
+    const uint64_t nw = nwords64(num_bits);
+    for (int g = 0; g < G; g++)
+        if (!d_words[g] || (n[g] && !d_keys[g])) return fail(LSMB_EINVAL, "null device pointer (shard %d)", g);
+    // 1. every shard's partial build, enqueued on its own stream (asynchronous)
+    for (int g = 0; g < G; g++) {
+        lsmb_ctx* c = m->ctx[g];
+        DevGuard dg(c->dev);
+        HIP_TRY(hipEventRecord(m->t0[g], c->st));
+        if (n[g] && k) {
+            KeyBatch kb{(const uint8_t*)d_keys[g], nullptr, key_len, key_len ? n[g] : 1};
+            if (int rc = build_dev(c, kb, num_bits, k, (uint32_t*)d_words[g], c->st)) return rc;
+        }
+        HIP_TRY(hipEventRecord(m->t1[g], c->st));
+        HIP_TRY(hipEventRecord(m->ev_built[g], c->st));
+    }
+    // 2. OR reduce-scatter by peer loads, 3. all-gather
+    std::vector<uint64_t*> part(G);
+    for (int g = 0; g < G; g++) part[g] = (uint64_t*)d_words[g];
+    if (G > 1) {
+        if (int rc = merge_reduce_scatter(m, part.data(), nw)) return rc;
+        if (int rc = merge_all_gather(m, part.data(), nw)) return rc;
+    }
+    for (int g = 0; g < G; g++) {
+        DevGuard dg(m->ctx[g]->dev);
+        HIP_TRY(hipEventRecord(m->t2[g], m->ctx[g]->st));
+    }
+    m->timed = true;
+    return sync_all(m);
+}
+
+int lsmb_multi_build_block(lsmb_multi* m, const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
+                           uint32_t num_bits, uint32_t k, uint8_t* block, uint64_t block_len) {
+    if (!m || !block) return fail(LSMB_EINVAL, "null argument");
+    if (int rc = check_filter(num_bits, k)) return rc;
+    const uint64_t nw = nwords64(num_bits);
+    if (block_len < 12 + 8 * nw) return fail(LSMB_EINVAL, "block buffer too small");
+    if (n && !offsets && !data && key_len) return fail(LSMB_EINVAL, "null keys");
+    if (n && offsets)
+        for (uint64_t i = 0; i < n; i++)
+            if (offsets[i + 1] < offsets[i]) return fail(LSMB_EINVAL, "offsets not non-decreasing at %llu", (unsigned long long)i);
+    // header of BloomFilter::serialize (src/bloom/mod.rs:102-115)
+    const uint32_t hdr[3] = {k, num_bits, (uint32_t)nw};
+    for (int i = 0; i < 3; i++)
+        for (int b = 0; b < 4; b++) block[4 * i + b] = (uint8_t)(hdr[i] >> (8 * b));
+    if (n == 0 || k == 0) {
+        memset(block + 12, 0, nw * 8);
+        return LSMB_OK;
+    }
+    const int G = shards(m);
+    std::vector<uint64_t*> part(G);
+    // 1. per shard (own thread: the H2D loops run in parallel over G PCIe links):
+    //    zeroed words, chunked H2D of the shard's keys overlapped with its build
+    if (!offsets && key_len == 0) n = 1;  // every key is the empty key: one insert
+    int rc = for_shards(m, [&](int g) -> int {
+        lsmb_ctx* c = m->ctx[g];
+        HIP_TRY(m->words[g].ensure(std::max<uint64_t>(nw, 2) * 8));
+        part[g] = (uint64_t*)m->words[g].p;
+        HIP_TRY(hipEventRecord(m->t0[g], c->st));
+        HIP_TRY(hipMemsetAsync(part[g], 0, nw * 8, c->st));
+        const uint64_t lo = n * g / G, hi = n * (g + 1) / G;
+        if (hi > lo) {
+            if (offsets) {
+                if (int r = host_build_dev(c, data, offsets + lo, 0, hi - lo, num_bits, k, (uint32_t*)part[g])) return r;
+            } else {
+                if (int r = host_build_dev(c, data + lo * key_len, nullptr, key_len, hi - lo, num_bits, k,
+                                           (uint32_t*)part[g]))
+                    return r;
+            }
+        }
+        HIP_TRY(hipEventRecord(m->t1[g], c->st));
+        HIP_TRY(hipEventRecord(m->ev_built[g], c->st));
+        return LSMB_OK;
+    });
+    if (rc) return rc;
+    // 2. OR reduce-scatter (peer loads); 3. each shard copies its merged slice
+    //    into the block body (no all-gather: the host only needs each slice once)
+    if (G > 1)
+        if (int r = merge_reduce_scatter(m, part.data(), nw)) return r;
+    rc = for_shards(m, [&](int g) -> int {
+        lsmb_ctx* c = m->ctx[g];
+        uint64_t lo, hi;
+        slice_of(nw, G, g, &lo, &hi);
+        if (hi > lo)
+            HIP_TRY(hipMemcpyAsync(block + 12 + lo * 8, part[g] + lo, (hi - lo) * 8, hipMemcpyDeviceToHost, c->st));
+        HIP_TRY(hipEventRecord(m->t2[g], c->st));
+        HIP_TRY(hipStreamSynchronize(c->st));
+        return check_device_error(c);
+    });
+    m->timed = rc == LSMB_OK;
+    return rc;
+}
+
+int lsmb_multi_last_ms(lsmb_multi* m, float* out3) {
+    if (!m || !out3) return fail(LSMB_EINVAL, "null argument");
+    if (!m->timed) return fail(LSMB_EINVAL, "no multi-GPU build on this handle");
+    float tot = 0.f, bld = 0.f;
+    for (int g = 0; g < shards(m); g++) {
+        DevGuard dg(m->ctx[g]->dev);
+        float a = 0.f, b = 0.f;
+        HIP_TRY(hipEventElapsedTime(&a, m->t0[g], m->t2[g]));
+        HIP_TRY(hipEventElapsedTime(&b, m->t0[g], m->t1[g]));
+        tot = std::max(tot, a);
+        bld = std::max(bld, b);
+    }
+    out3[0] = tot;
+    out3[1] = bld;
+    out3[2] = tot - bld;
+    return LSMB_OK;
+}
+
+}  // extern "C"

@@ -11,7 +11,10 @@ src/bloom/mod.rs, src/bloom/builder.rs) so tests read like the reference's own:
 
 Batched work (BloomFilterBuilder.build, probe_batch) runs on the GPU through
 the C ABI; it raises if the HIP library or a gfx950 device is missing — there
-is no CPU fallback.  Device-resident entry points take torch tensors.
+is no CPU fallback.  The one host path is the library's own, size-bounded:
+builds of at most host_max_keys() keys (an SST flush at the reference's
+default 1 000-key sizing) run its native per-key loop and need no GPU.
+Device-resident entry points take torch tensors.
 """
 import ctypes
 import os
@@ -75,7 +78,18 @@ SIGNATURES = {
     "lsmb_fset_live_mask": (ctypes.c_uint64, [vp]),
     "lsmb_fset_probe": (ctypes.c_int, [vp, u8p, u64p, ctypes.c_uint32, ctypes.c_uint64, u64p]),
     "lsmb_fset_probe_dev": (ctypes.c_int, [vp, vp, vp, ctypes.c_uint32, ctypes.c_uint64, vp, vp]),
-    "lsmb_build_strategy": (ctypes.c_char_p, [ctypes.c_uint32, ctypes.c_uint64]),
+    "lsmb_build_strategy": (ctypes.c_char_p, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]),
+    "lsmb_host_max_keys": (ctypes.c_uint64, []),
+    "lsmb_set_host_max_keys": (None, [ctypes.c_uint64]),
+    "lsmb_multi_open": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    "lsmb_multi_close": (None, [vp]),
+    "lsmb_multi_size": (ctypes.c_int, [vp]),
+    "lsmb_multi_ctx": (vp, [vp, ctypes.c_int]),
+    "lsmb_multi_build_fixed_dev": (ctypes.c_int, [vp, ctypes.POINTER(vp), u64p, ctypes.c_uint32, ctypes.c_uint32,
+                                                  ctypes.c_uint32, ctypes.POINTER(vp)]),
+    "lsmb_multi_build_block": (ctypes.c_int, [vp, u8p, u64p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
+                                              ctypes.c_uint32, u8p, ctypes.c_uint64]),
+    "lsmb_multi_last_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_float)]),
     "lsmb_last_build_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_float)]),
     "lsmb_set_timing": (ctypes.c_int, [vp, ctypes.c_int]),
 }
@@ -389,8 +403,74 @@ class FilterSet:
                                          vp(out.data_ptr()), Context._stream(stream)))
 
 
-def build_strategy(num_bits, n):
-    return lib().lsmb_build_strategy(num_bits, n).decode()
+def build_strategy(num_bits, n, k=7):
+    """Device build strategy for (num_bits, k, n): lds / tiled / partition / atomic."""
+    return lib().lsmb_build_strategy(num_bits, k, n).decode()
+
+
+def host_max_keys():
+    """Host-memory builds of at most this many keys run the library's host loop."""
+    return int(lib().lsmb_host_max_keys())
+
+
+def set_host_max_keys(n):
+    lib().lsmb_set_host_max_keys(int(n))
+
+
+class Multi:
+    """One process, several GPUs (lsmb_multi): a sharded build merged by an
+    OR reduce-scatter over xGMI peer loads.  `devices` may repeat."""
+
+    def __init__(self, devices):
+        devices = list(devices)
+        h = vp()
+        arr = (ctypes.c_int * len(devices))(*devices)
+        _check(lib().lsmb_multi_open(ctypes.byref(h), arr, len(devices)))
+        self.h = h
+        self.devices = devices
+
+    def close(self):
+        if self.h:
+            lib().lsmb_multi_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def size(self):
+        return int(lib().lsmb_multi_size(self.h))
+
+    def build_fixed_dev(self, keys, key_len, num_bits, k, words):
+        """keys / words: per-shard torch tensors on the shards' devices; every
+        words[g] ends holding the merged filter."""
+        G = len(keys)
+        karr = (vp * G)(*[vp(t.data_ptr()) for t in keys])
+        warr = (vp * G)(*[vp(t.data_ptr()) for t in words])
+        n = np.array([t.numel() // key_len if key_len else t.shape[0] for t in keys], dtype=np.uint64)
+        _check(lib().lsmb_multi_build_fixed_dev(self.h, karr, _p(n, u64p), key_len, num_bits, k, warr))
+
+    def build_block(self, data, num_bits, k, offsets=None, key_len=0, out=None):
+        data = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+        if offsets is not None:
+            offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+            n, op = offsets.size - 1, _p(offsets, u64p)
+        else:
+            n, op = (data.size // key_len if key_len else 0), None
+        if out is None:
+            out = np.empty(serialized_size(num_bits), dtype=np.uint8)
+        if data.size == 0:
+            data = np.zeros(1, np.uint8)
+        _check(lib().lsmb_multi_build_block(self.h, _p(data, u8p), op, key_len, n, num_bits, k, _p(out, u8p),
+                                            out.size))
+        return out
+
+    def last_ms(self):
+        a = (ctypes.c_float * 3)()
+        _check(lib().lsmb_multi_last_ms(self.h, a))
+        return tuple(a)
 
 
 _default_ctx = None
@@ -482,20 +562,34 @@ class BloomFilterBuilder:
         self._data += bytes(key)
         self._offs.append(len(self._data))
 
+    def _ctx_for(self, n):
+        """The device context a build of n keys needs: None at or below the
+        library's host threshold (SST-sized flushes stay on the host, no GPU
+        required), else the GPU context (raises without a gfx950 device)."""
+        if n <= host_max_keys():
+            return None
+        return self._ctx or default_context()
+
     def build(self):
         f = self._filter
-        if len(self._offs) > 1:
-            ctx = self._ctx or default_context()
+        n = len(self._offs) - 1
+        if n:
+            ctx = self._ctx_for(n)
             offs = np.array(self._offs, dtype=np.uint64)
-            data = np.frombuffer(bytes(self._data), dtype=np.uint8)
-            ctx.build_var(data, offs, f._nb, f._k, f.bits)
+            data = np.frombuffer(bytes(self._data) or b"\0", dtype=np.uint8)
+            _check(lib().lsmb_build_var(ctx.h if ctx else None, _p(data, u8p), _p(offs, u64p), n, f._nb, f._k,
+                                        _p(f.bits, u64p)))
         return f
 
     def build_serialized(self):
-        """build().serialize() in one GPU call (lsmb_build_block): the bloom block
+        """build().serialize() in one call (lsmb_build_block): the bloom block
         SSTableBuilder::finish writes (src/sstable/builder.rs:177-179)."""
         f = self._filter
-        ctx = self._ctx or default_context()
+        n = len(self._offs) - 1
+        ctx = self._ctx_for(n)
         offs = np.array(self._offs, dtype=np.uint64)
-        data = np.frombuffer(bytes(self._data), dtype=np.uint8)
-        return ctx.build_block(data, f._nb, f._k, offsets=offs).tobytes()
+        data = np.frombuffer(bytes(self._data) or b"\0", dtype=np.uint8)
+        out = np.empty(serialized_size(f._nb), dtype=np.uint8)
+        _check(lib().lsmb_build_block(ctx.h if ctx else None, _p(data, u8p), _p(offs, u64p), 0, n, f._nb, f._k,
+                                      _p(out, u8p), out.size))
+        return out.tobytes()

@@ -24,6 +24,12 @@ def _slices(n, world):
     return per
 
 
+def _host_staged(words, group):
+    """gloo moves host memory only: device words are staged through it (the
+    one-GPU multi-rank tests); RCCL (nccl) works on device memory directly."""
+    return words.is_cuda and dist.get_backend(group) == "gloo"
+
+
 def or_reduce_scatter_(words, group=None, ctx=None):
     """Returns (slice_tensor, start_word): this rank's merged slice of the filter."""
     world = dist.get_world_size(group)
@@ -35,8 +41,13 @@ def or_reduce_scatter_(words, group=None, ctx=None):
         buf[:n].copy_(words)
     else:
         buf = words
-    recv = torch.empty_like(buf)
-    dist.all_to_all_single(recv, buf, group=group)
+    if _host_staged(words, group):
+        recv_h = torch.empty(buf.shape, dtype=buf.dtype)
+        dist.all_to_all_single(recv_h, buf.cpu(), group=group)
+        recv = recv_h.to(words.device)
+    else:
+        recv = torch.empty_like(buf)
+        dist.all_to_all_single(recv, buf, group=group)
     mine = torch.empty(per, dtype=words.dtype, device=words.device)
     if words.is_cuda and ctx is not None:
         mine.zero_()
@@ -57,6 +68,11 @@ def or_allreduce_(words, group=None, ctx=None):
     n = words.numel()
     mine, _ = or_reduce_scatter_(words, group, ctx)
     per = mine.numel()
+    if _host_staged(words, group):
+        out = torch.empty(per * world, dtype=words.dtype)
+        dist.all_gather_into_tensor(out, mine.cpu(), group=group)
+        words.copy_(out[:n])
+        return words
     if per * world == n and words.is_contiguous():
         dist.all_gather_into_tensor(words, mine, group=group)  # no staging copy (C5: 2^26 words)
         return words

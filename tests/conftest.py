@@ -18,3 +18,20 @@ def pytest_configure(config):
 def oracle():
     import oracle_ct
     return oracle_ct.load()
+
+
+@pytest.fixture(autouse=True)
+def _gpu_tests_use_the_gpu(request):
+    """GPU tests keep every build on the device: host-memory builds at or below
+    lsmb_host_max_keys() would otherwise take the library's host loop (the
+    threshold's own tests set it explicitly)."""
+    if request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    import lsmbloom
+    old = lsmbloom.host_max_keys()
+    lsmbloom.set_host_max_keys(0)
+    try:
+        yield
+    finally:
+        lsmbloom.set_host_max_keys(old)

@@ -8,6 +8,7 @@
 
 #include <functional>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../storage-engine_amd/cpp/lsm_bloom.hpp"
@@ -36,7 +37,8 @@ static bool throws(F&& f) {
     return false;
 }
 
-static void run(const char* name, const std::function<void()>& f) {
+static void run(const std::string& name_s, const std::function<void()>& f) {
+    const char* name = name_s.c_str();
     g_run++;
     try {
         f();
@@ -187,9 +189,12 @@ int main(int argc, char** argv) {
         CHECK(bf2.num_hashes() == bf.num_hashes() && bf2.num_bits() == bf.num_bits());
     });
 
-    if (gpu) {
-        // ---- the builder path (SSTableBuilder -> BloomFilterBuilder, src/sstable/builder.rs:74,93,177)
-        run("builder matches single-key inserts (builder.rs:14-28)", [] {
+    // ---- the builder path (SSTableBuilder -> BloomFilterBuilder, src/sstable/builder.rs:74,93,177).
+    // Run twice: with the default host threshold (SST-sized builds take the
+    // library's host loop; no GPU needed) and, on a GPU, with the threshold at
+    // 0 (every build on the device).  The bits must be the same both ways.
+    auto builder_tests = [&](const char* tag) {
+        run(std::string("builder matches single-key inserts (builder.rs:14-28) [") + tag + "]", [] {
             BloomFilterBuilder b(1000, 0.01);  // SSTableBuilder::new sizing
             BloomFilter ref(1000, 0.01);
             char k[16];
@@ -202,19 +207,21 @@ int main(int argc, char** argv) {
             CHECK(bf.words() == ref.words());
             CHECK(bf.serialize() == ref.serialize());
         });
-        run("build_serialized == build().serialize() (SSTableBuilder::finish, builder.rs:177-179)", [] {
-            BloomFilterBuilder b(1000, 0.01), b2(1000, 0.01);
-            char k[16];
-            for (int i = 0; i < 700; i++) {
-                snprintf(k, sizeof k, "blk_%06d", i);
-                b.add_key(k);
-                b2.add_key(k);
-            }
-            BloomFilterBuilder empty(1000, 0.01);
-            CHECK(b.build_serialized() == b2.build().serialize());
-            CHECK(empty.build_serialized() == BloomFilter(1000, 0.01).serialize());
-        });
-        run("sstable bloom: existing found, absent rejected (integration_tests.rs:12-59)", [] {
+        run(std::string("build_serialized == build().serialize() (SSTableBuilder::finish, builder.rs:177-179) [") + tag +
+                "]",
+            [] {
+                BloomFilterBuilder b(1000, 0.01), b2(1000, 0.01);
+                char k[16];
+                for (int i = 0; i < 700; i++) {
+                    snprintf(k, sizeof k, "blk_%06d", i);
+                    b.add_key(k);
+                    b2.add_key(k);
+                }
+                BloomFilterBuilder empty(1000, 0.01);
+                CHECK(b.build_serialized() == b2.build().serialize());
+                CHECK(empty.build_serialized() == BloomFilter(1000, 0.01).serialize());
+            });
+        run(std::string("sstable bloom: existing found, absent rejected (integration_tests.rs:12-59) [") + tag + "]", [] {
             BloomFilterBuilder b(1000, 0.01);
             char k[16];
             for (int i = 0; i < 100; i++) {
@@ -227,6 +234,43 @@ int main(int argc, char** argv) {
                 CHECK(bf.may_contain(k));
             }
         });
+    };
+    builder_tests("host path");
+
+    if (gpu) {
+        const uint64_t thr = lsmb_host_max_keys();
+        lsmb_set_host_max_keys(0);
+        builder_tests("gpu path");
+        run("flush + compaction threads build at once, one context each (scheduler.rs:37)", [] {
+            // Context::shared() is thread_local: the two threads never share
+            // staging buffers.  100 k keys each: partition-free LDS builds.
+            auto work = [](int seed, std::vector<uint8_t>* out) {
+                BloomFilterBuilder b(100000, 0.01);
+                char k[24];
+                for (int i = 0; i < 100000; i++) {
+                    snprintf(k, sizeof k, "t%d_%08d", seed, i);
+                    b.add_key(k);
+                }
+                *out = b.build_serialized();
+            };
+            std::vector<uint8_t> a1, b1, a2, b2;
+            for (int rep = 0; rep < 3; rep++) {
+                std::thread t1(work, 1, &a1), t2(work, 2, &b1);
+                t1.join();
+                t2.join();
+            }
+            work(1, &a2);
+            work(2, &b2);
+            CHECK(a1 == a2 && b1 == b2);
+            BloomFilter ref(100000, 0.01);
+            char k[24];
+            for (int i = 0; i < 100000; i++) {
+                snprintf(k, sizeof k, "t1_%08d", i);
+                ref.insert(k);
+            }
+            CHECK(a1 == ref.serialize());
+        });
+        lsmb_set_host_max_keys(thr);
         run("sstable bloom fpr, batched probe (integration_tests.rs:66-113)", [] {
             BloomFilterBuilder b(1000, 0.01);
             char k[16];

@@ -1,0 +1,282 @@
+"""Multi-GPU paths on the GPU box.
+
+The box has one MI355X, so every multi-shard test here runs its shards on
+device 0: the same kernels, the same merge, with the "peer" reads served
+locally.  The 8-GPU runs are the driver's (bench.py --gpus 8).
+
+* lsmb_multi (one process, several GPUs): sharded device build + OR
+  reduce-scatter by peer loads + all-gather; sharded host-keys build straight
+  into the serialized block.  Every word vs the single-process oracle build.
+* torch.distributed ranks (one process per GPU): two ranks on cuda:0 build
+  partials with the HIP kernels and merge over gloo through
+  lsmbloom.dist.or_allreduce_(..., ctx=...), i.e. the device OR kernel
+  (lsmb_or_reduce_dev) — the path the RCCL bench takes, with gloo moving the
+  bytes because RCCL refuses two ranks on one device.
+* bench.py --gpus 2 launching its own ranks (the driver's form).
+* One context used from two streams (the partition workspace guard), and a
+  filter-set add on one context while another context's builds are queued.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+import threading
+import time
+
+import numpy as np
+import pytest
+
+import keygen
+import lsmbloom
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+    assert torch.cuda.is_available()
+    return torch
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = lsmbloom.Context(0)
+    yield c
+    c.close()
+
+
+def _u64(t):
+    return t.cpu().numpy().view(np.uint64)
+
+
+@pytest.mark.parametrize("G,n,filter_n", [(2, 2_000_000, 50_000_000),   # partition
+                                          (3, 1_000_001, 1_000_000),    # tiled, ragged shards
+                                          (4, 40_000, 40_000),          # lds, odd word count
+                                          (2, 3, 10_000_000)])          # atomic, shards of 1-2 keys
+def test_multi_build_fixed_dev_equals_oracle(torch, oracle, G, n, filter_n):
+    nb, k = lsmbloom.params(filter_n, 0.01)
+    nw = lsmbloom.num_words(nb)
+    dev = torch.device("cuda:0")
+    m = lsmbloom.Multi([0] * G)
+    try:
+        assert m.size() == G
+        keys, words = [], []
+        host = keygen.key16(0x5EED0001, 0, n)
+        for g in range(G):
+            lo, hi = n * g // G, n * (g + 1) // G
+            keys.append(torch.from_numpy(np.ascontiguousarray(host[lo:hi])).to(dev))
+            words.append(torch.zeros(nw, dtype=torch.int64, device=dev))
+        m.build_fixed_dev(keys, 16, nb, k, words)
+        ref = oracle.build_fixed_mt(host, 16, nb, k, 8)
+        for g in range(G):
+            assert np.array_equal(_u64(words[g]), ref), "shard %d's merged filter differs" % g
+        tot, bld, mrg = m.last_ms()
+        assert tot >= bld >= 0 and mrg >= 0
+    finally:
+        m.close()
+
+
+def test_multi_build_fixed_dev_or_accumulates(torch, oracle):
+    # pre-existing bits in any shard's words survive the merge (OR-accumulate)
+    nb, k = lsmbloom.params(3_000_000, 0.01)
+    nw = lsmbloom.num_words(nb)
+    dev = torch.device("cuda:0")
+    pre = oracle.build_fixed(keygen.key16(7, 0, 1000), 16, nb, k)
+    host = keygen.key16(0x5EED0001, 0, 300_000)
+    m = lsmbloom.Multi([0, 0])
+    try:
+        keys = [torch.from_numpy(np.ascontiguousarray(host[:100_000])).to(dev),
+                torch.from_numpy(np.ascontiguousarray(host[100_000:])).to(dev)]
+        words = [torch.from_numpy(pre.view(np.int64).copy()).to(dev), torch.zeros(nw, dtype=torch.int64, device=dev)]
+        m.build_fixed_dev(keys, 16, nb, k, words)
+        ref = oracle.build_fixed(host, 16, nb, k, words=pre.copy())
+        assert np.array_equal(_u64(words[0]), ref) and np.array_equal(_u64(words[1]), ref)
+    finally:
+        m.close()
+
+
+@pytest.mark.parametrize("G", [1, 2, 3])
+def test_multi_build_block_fixed_and_varlen(oracle, G):
+    m = lsmbloom.Multi([0] * G)
+    try:
+        n = 3_000_000
+        nb, k = lsmbloom.params(n, 0.01)
+        keys = keygen.key16(0x5EED0001, 0, n)
+        blk = m.build_block(keys, nb, k, key_len=16)
+        ref = oracle.serialize(oracle.build_fixed_mt(keys, 16, nb, k, 8), nb, k)
+        assert bytes(blk) == bytes(ref)
+        data, offs = keygen.varlen(400_000)
+        nb2, k2 = lsmbloom.params(400_000, 0.01)
+        blk2 = m.build_block(data, nb2, k2, offsets=offs)
+        assert bytes(blk2) == bytes(oracle.serialize(oracle.build_var(data, offs, nb2, k2), nb2, k2))
+        # degenerate runs: no keys, and every key empty (one insert of b"")
+        assert bytes(m.build_block(np.zeros(0, np.uint8), nb, k, key_len=16)) == \
+            bytes(oracle.serialize(np.zeros(lsmbloom.num_words(nb), np.uint64), nb, k))
+        empty_ref = oracle.serialize(oracle.build_var(b"", np.zeros(2, np.uint64), nb2, k2), nb2, k2)
+        assert bytes(m.build_block(np.zeros(0, np.uint8), nb2, k2, offsets=np.zeros(5, np.uint64))) == \
+            bytes(empty_ref)
+    finally:
+        m.close()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _dist_worker(rank, world, port, n, filter_n, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, os.path.join(ROOT, "storage-engine_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch
+    import torch.distributed as dist
+
+    import lsmbloom
+    from lsmbloom import dist as ldist
+    lsmbloom.set_host_max_keys(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda:0")
+        ctx = lsmbloom.Context(0)
+        nb, k = lsmbloom.params(filter_n, 0.01)
+        lo, hi = n * rank // world, n * (rank + 1) // world
+        keys = torch.empty((hi - lo, 16), dtype=torch.uint8, device=dev)
+        ctx.gen_key16_dev(0x5EED0001, lo, hi - lo, keys)
+        words = torch.zeros(lsmbloom.num_words(nb), dtype=torch.int64, device=dev)
+        ctx.build_fixed_dev(keys, 16, hi - lo, nb, k, words)
+        part = words.clone()
+        mine, start = ldist.or_reduce_scatter_(part, ctx=ctx)
+        ldist.or_allreduce_(words, ctx=ctx)
+        torch.cuda.synchronize()
+        q.put((rank, words.cpu().numpy().view(np.uint64).copy(), mine.cpu().numpy().view(np.uint64).copy(), start))
+        ctx.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,filter_n", [(2, 3_000_000, 30_000_000), (3, 500_001, 500_001)])
+def test_dist_or_allreduce_device_path(oracle, world, n, filter_n):
+    import torch.multiprocessing as mp
+    mpc = mp.get_context("spawn")
+    q = mpc.Queue()
+    port = _free_port()
+    procs = [mpc.Process(target=_dist_worker, args=(r, world, port, n, filter_n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    nb, k = lsmbloom.params(filter_n, 0.01)
+    ref = oracle.build_fixed_mt(keygen.key16(0x5EED0001, 0, n), 16, nb, k, 8)
+    for rank, words, mine, start in res:
+        assert np.array_equal(words, ref), "rank %d merged filter differs" % rank
+        end = min(start + mine.size, ref.size)
+        assert np.array_equal(mine[: end - start], ref[start:end])
+
+
+def test_bench_launches_its_own_ranks():
+    """`python bench.py --gpus 2` (no torchrun) starts two ranks itself; here
+    over gloo, both on cuda:0.  The line must say n_gpus 2, carry the split
+    build / OR-allreduce timing, and the rank-0 word-for-word self-check."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
+           "--global-keys", "8000000", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-e2e",
+           "--no-varlen", "--no-exact10", "--probe-keys", "200000"]
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1, r.stdout
+    out = json.loads(line[0])
+    assert out["n_gpus"] == 2 and out["config"]["global_keys"] == 8_000_000
+    assert out["scaling"] == "strong" and out["config"]["keys_per_gpu"] == 4_000_000
+    assert out["multi_gpu_merged_equals_single_gpu_build"] is True
+    assert out["step_split"]["or_allreduce_ms"] > 0 and out["step_split"]["build_ms"] > 0
+    assert out["probe"]["member_rows_all_hit"] is True
+
+
+def test_bench_refuses_world_mismatch():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 2 and "WORLD_SIZE" in r.stderr
+
+
+def test_one_context_two_streams(torch, oracle):
+    """the partition workspace is shared by every build on a
+    context; a build issued on another stream must wait for the previous one
+    (build_dev's ws_done event) instead of overwriting its regions."""
+    ctx = lsmbloom.Context(0)
+    try:
+        dev = torch.device("cuda:0")
+        n = 1_500_000
+        nb, k = lsmbloom.params(40_000_000, 0.01)
+        assert lsmbloom.build_strategy(nb, n) == "partition"
+        ka = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+        kb = torch.empty_like(ka)
+        ctx.gen_key16_dev(11, 0, n, ka)
+        ctx.gen_key16_dev(22, 0, n, kb)
+        torch.cuda.synchronize()
+        s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        wa = torch.zeros(lsmbloom.num_words(nb), dtype=torch.int64, device=dev)
+        wb = torch.zeros_like(wa)
+        torch.cuda.synchronize()
+        for _ in range(3):  # alternate streams back to back, no host sync between
+            ctx.build_fixed_dev(ka, 16, n, nb, k, wa, stream=s1.cuda_stream)
+            ctx.build_fixed_dev(kb, 16, n, nb, k, wb, stream=s2.cuda_stream)
+        torch.cuda.synchronize()
+        ctx.sync()
+        assert np.array_equal(_u64(wa), oracle.build_fixed_mt(keygen.key16(11, 0, n), 16, nb, k, 8))
+        assert np.array_equal(_u64(wb), oracle.build_fixed_mt(keygen.key16(22, 0, n), 16, nb, k, 8))
+    finally:
+        ctx.close()
+
+
+def test_fset_add_does_not_wait_for_other_contexts(torch, oracle):
+    """a filter-set add/remove on one context (the read
+    path) must not stall on another context's queued builds (flush /
+    compaction): it waits for its own set's probes only."""
+    dev = torch.device("cuda:0")
+    a, b = lsmbloom.Context(0), lsmbloom.Context(0)
+    try:
+        n = 20_000_000
+        nb, k = lsmbloom.params(n, 0.01)
+        keys = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+        a.gen_key16_dev(3, 0, n, keys, stream=a_stream(a))
+        words = torch.zeros(lsmbloom.num_words(nb), dtype=torch.int64, device=dev)
+        fs = lsmbloom.FilterSet(b)
+        f = lsmbloom.BloomFilter.new(1000, 0.01)
+        for i in range(100):
+            f.insert(b"key_%05d" % i)
+        fs.add_filter(f, b"key_00000", b"key_00099")  # warm-up: slot buffer, stream, staging
+        fs.probe_keys([b"key_00005", b"zzz"])
+        a.sync()
+        # queue ~30 builds on context a's own stream, then time an add on b
+        t0 = time.perf_counter()
+        for _ in range(30):
+            a.build_fixed_dev(keys, 16, n, nb, k, words, stream=a_stream(a))
+        t_enq = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        slot = fs.add_filter(f, b"key_00000", b"key_00099")
+        got = fs.probe_keys([b"key_00005", b"zzz"])
+        t_add = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        a.sync()
+        t_rest = time.perf_counter() - t0
+        assert (int(got[0]) >> slot) & 1 == 1 and int(got[1]) == 0
+        # the add + probe finished while most of a's queue was still running
+        assert t_add < 0.5 * (t_add + t_rest), (t_enq, t_add, t_rest)
+        fs.close()
+    finally:
+        a.close()
+        b.close()
+
+
+def a_stream(c):
+    """The context's own stream (NULL selects it)."""
+    return 0
