@@ -42,6 +42,9 @@
 #ifndef LSMB_ABL
 #define LSMB_ABL 0
 #endif
+#ifndef LSMB_PIPE
+#define LSMB_PIPE 0
+#endif
 #ifndef LSMB_APPLY_U
 #define LSMB_APPLY_U 8  // pass B: 16-B region loads in flight per lane
 #endif
@@ -162,8 +165,14 @@ __device__ __forceinline__ void or_pos_global(uint32_t* gw, uint32_t b, uint32_t
     atomicOr(gw + (p >> 5), 1u << (p & 31));
 }
 
+// Three 20-bit offsets in one u64: x | y << 20 | z << 40, built from 32-bit
+// shift-or instructions (no 64-bit shifts).
+__device__ __forceinline__ uint2 pack3w(uint32_t x, uint32_t y, uint32_t z) {
+    return make_uint2(x | (y << 20), (y >> 12) | (z << 8));
+}
 __device__ __forceinline__ uint64_t pack3(uint32_t x, uint32_t y, uint32_t z) {
-    return (uint64_t)x | ((uint64_t)y << 20) | ((uint64_t)z << 40);
+    const uint2 w = pack3w(x, y, z);
+    return ((uint64_t)w.y << 32) | w.x;
 }
 
 // Pass A (k_bin): hash keys, bin every position's 20-bit in-slice offset by
@@ -206,6 +215,8 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
     const uint32_t k = EXACT ? (uint32_t)KMAX : k_;
     const uint32_t R = a.ring, R4 = 4 * a.ring, nb = a.nb;
     uint32_t* fill = sm + (size_t)(nb + 1) * R;  // nb + 1 fill words (the last: sink)
+    // per-wave flush job tables, 16-B aligned after the fill words
+    uint4* jobtab = reinterpret_cast<uint4*>(sm + ((((size_t)(nb + 1) * (R + 1)) + 3) & ~(size_t)3));
     const uint32_t tid = threadIdx.x, w = blockIdx.x, lane = tid & 63, wave = tid >> 6;
     for (uint32_t i = tid; i <= nb; i += kBinBlock) fill[i] = 0;
     // Workgroup w's regions as a raw buffer: a store at an offset past
@@ -236,9 +247,15 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
         for (int q = 0; q < KMAX; q++) {
             if (EXACT || (uint32_t)q < k) {
                 const uint32_t lp = walk.pos() - (FULL ? 0u : (a.b0 << kSliceLog2));
-                out[q] = ok && (FULL || lp < sink) ? lp : sink;
+                out[q] = (FULL || lp < sink) ? lp : sink;
                 if (q + 1 < KMAX) walk.next(md);
             }
+        }
+        // lanes past the key range (the last phases only): sink positions
+        if (__builtin_expect(__ballot(!ok) != 0, 0)) {
+#pragma unroll
+            for (int q = 0; q < KMAX; q++)
+                if (!ok && (EXACT || (uint32_t)q < k)) out[q] = sink;
         }
     };
     // a lane's keys of phase `it`: key_index(it) + j, j < PER
@@ -254,7 +271,15 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
     // register copy forces a vmcnt drain).  gfx9 retires loads and stores in
     // one in-order vmcnt queue: a key load completes only after every older
     // region store, so the distance must cover the store round trip too.
+    // LSMB_PIPE=1 (measurement variant): a key goes through three phases —
+    // hashed in phase it-2, walked in phase it-1, claimed in phase it — so
+    // every phase runs two independent dependency chains per lane.  Measured
+    // slower (pass A 1.05 -> 1.10 ms at C2); the
+    // default hashes and walks key it+1 in one chain during phase it.
+    constexpr bool kPipe = LSMB_PIPE != 0;
     Pre pb0[PER], pb1[PER], pb2[PER], pb3[PER];  // phase m's keys live in pb[m % 4]
+    bool nok[PER];
+    H128 nh[PER];  // kPipe: key it+1's hash
 #pragma unroll
     for (int j = 0; j < PER; j++) {
         const bool ok = key_ok(0, j);
@@ -262,15 +287,27 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
         const H128 h = ok ? src.hash_pre(p, key_index(0) + j) : H128{0, 0};
         walk_positions(h, ok, pos + j * KMAX);
         kinc[j] = ok ? kInc : 0u;
+        if constexpr (kPipe) {
+            nok[j] = key_ok(1, j);
+            const Pre p1 = src.fetch(key_index(1) + j, nok[j]);
+            nh[j] = nok[j] ? src.hash_pre(p1, key_index(1) + j) : H128{0, 0};
+        }
     }
-    fetch_keys(1, pb1);
-    fetch_keys(2, pb2);
-    fetch_keys(3, pb3);
-    fetch_keys(4, pb0);
+    if constexpr (kPipe) {
+        fetch_keys(2, pb2);
+        fetch_keys(3, pb3);
+        fetch_keys(4, pb0);
+        fetch_keys(5, pb1);
+    } else {
+        fetch_keys(1, pb1);
+        fetch_keys(2, pb2);
+        fetch_keys(3, pb3);
+        fetch_keys(4, pb0);
+    }
     __syncthreads();
 
-    // One phase: claim key it's positions, hash key it+1 (from `pre`) and
-    // reload `pre` with key it+1+kAhead, store the entries, flush.
+    // One phase: claim key it's positions, hash and walk key it+1 (from
+    // `pre`) and reload `pre` with key it+1+kAhead, store the entries, flush.
     auto phase = [&](uint64_t it, Pre (&pre)[PER]) __attribute__((always_inline)) {
         // Claims for this phase's keys, back to back.
         uint32_t got[NP];
@@ -288,54 +325,99 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
                 }
             }
         }
-        // Next phase's keys: hash while the claims are in flight.
-        bool nok[PER];
-        H128 nh[PER];
+        // While the claims are in flight: hash and walk key it+1, pinned here
+        // (an empty asm that consumes the positions): otherwise the compiler
+        // sinks the whole hash + walk below the barrier, where every wave
+        // computes while none has LDS work, and the claims' round trip is
+        // exposed instead.
+        uint32_t npos[NP], nkinc[PER];
+        bool nok2[PER];
+        H128 nh2[PER];
 #pragma unroll
         for (int j = 0; j < PER; j++) {
-            nok[j] = key_ok(it + 1, j);
-            nh[j] = src.hash_pre(pre[j], key_index(it + 1) + j);
-        }
-        fetch_keys(it + 1 + kAhead, pre);
-        // Store the claimed entries (overflowing claims into the sink's slot 0).
-        uint32_t gmax = 0;
-#pragma unroll
-        for (int q = 0; q < NP; q++) {
-            if (EXACT || (uint32_t)q < k) {
-                const uint32_t b = pos[q] >> kSliceLog2;
-                uint32_t x = got[q] & 0xFFFFu;
-                x = min(x, x - R4);
-                const uint32_t tgt = got[q] < lim ? b * R4 + x : nb * R4;
-                if (LSMB_ABL & 2)
-                    gmax ^= tgt;
-                else if (FULL || pos[q] < sink)
-                    *(uint32_t*)((char*)sm + tgt) = pos[q] & kSliceMask;
-                if (!(LSMB_ABL & 2)) gmax = max(gmax, got[q]);
+            if constexpr (kPipe) {
+                walk_positions(nh[j], nok[j], npos + j * KMAX);
+                nkinc[j] = nok[j] ? kInc : 0u;
+                nok2[j] = key_ok(it + 2, j);
+                nh2[j] = src.hash_pre(pre[j], key_index(it + 2) + j);
+            } else {
+                const bool ok = key_ok(it + 1, j);
+                walk_positions(src.hash_pre(pre[j], key_index(it + 1) + j), ok, npos + j * KMAX);
+                nkinc[j] = ok ? kInc : 0u;
             }
         }
-        if (__builtin_expect(__ballot(gmax >= lim) != 0, 0)) {
+        fetch_keys(it + (kPipe ? 2 : 1) + kAhead, pre);
 #pragma unroll
-            for (int q = 0; q < NP; q++)
-                if ((EXACT || (uint32_t)q < k) && got[q] >= lim && pos[q] < sink) {
-                    or_pos_global(a.gw, a.b0 + (pos[q] >> kSliceLog2), pos[q] & kSliceMask);
-#ifdef LSMB_STATS
-                    atomicAdd(a.err + 9, 1u);
-#endif
+        for (int q = 0; q < NP; q++)
+            if (EXACT || (uint32_t)q < k) asm volatile("" ::"v"(npos[q]));
+        if constexpr (kPipe) {
+#pragma unroll
+            for (int j = 0; j < PER; j++)
+                asm volatile("" ::"v"((uint32_t)nh2[j].lo), "v"((uint32_t)(nh2[j].lo >> 32)), "v"((uint32_t)nh2[j].hi),
+                             "v"((uint32_t)(nh2[j].hi >> 32)));
+        }
+        // Store the claimed entries.  Fast path (every claim of the wave fits
+        // its ring): slot address = b * R4 + wrapped ring offset, one full-rate
+        // 24-bit multiply-add, no per-position select.  A wave with an
+        // overflowing claim (adversarial duplicates only) takes the checked
+        // path: overflowing claims skip the ring and set their bit with a
+        // global atomic (pass B reads the filter words after pass A, so the
+        // result is exact).
+        uint32_t gmax = 0;
+#pragma unroll
+        for (int q = 0; q < NP; q++)
+            if (EXACT || (uint32_t)q < k) gmax = max(gmax, got[q]);
+        auto slot = [&](int q) {
+            uint32_t x = got[q] & 0xFFFFu;
+            x = min(x, x - R4);
+            return __umul24(pos[q] >> kSliceLog2, R4) + x;
+        };
+        if (__builtin_expect(__ballot(gmax >= lim) == 0, 1)) {
+#pragma unroll
+            for (int q = 0; q < NP; q++) {
+                if (EXACT || (uint32_t)q < k) {
+                    if (LSMB_ABL & 2) continue;
+                    if (FULL || pos[q] < sink) *(uint32_t*)((char*)sm + slot(q)) = pos[q] & kSliceMask;
                 }
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < NP; q++) {
+                if ((EXACT || (uint32_t)q < k) && (FULL || pos[q] < sink)) {
+                    if (got[q] < lim) {
+                        *(uint32_t*)((char*)sm + slot(q)) = pos[q] & kSliceMask;
+                    } else if (pos[q] < sink) {  // (the sink's claims add 0: never past its ring)
+                        or_pos_global(a.gw, a.b0 + (pos[q] >> kSliceLog2), pos[q] & kSliceMask);
+#ifdef LSMB_STATS
+                        atomicAdd(a.err + 9, 1u);
+#endif
+                    }
+                }
+            }
         }
 #pragma unroll
+        for (int q = 0; q < NP; q++) pos[q] = npos[q];
+#pragma unroll
         for (int j = 0; j < PER; j++) {
-            walk_positions(nh[j], nok[j], pos + j * KMAX);
-            kinc[j] = nok[j] ? kInc : 0u;
+            kinc[j] = nkinc[j];
+            if constexpr (kPipe) {
+                nok[j] = nok2[j];
+                nh[j] = nh2[j];
+            }
         }
         lds_barrier();
 
-        // Flush: each owner lane writes its slice's full segment (usually
-        // none or one) to the region, 4 x 16 B.  The four stores are issued
-        // by every lane, at a dropped offset where there is nothing to write:
-        // with a static store count per phase the compiler's vmcnt waits for
-        // the prefetched keys stay counted (a conditional store would make
-        // them drain the latest phase's stores).
+        // Flush, wave-cooperative: every owner lane whose slice holds a full
+        // 24-entry segment posts it as a job {group addresses, region offset}
+        // in its wave's LDS job table; then four lanes write each job's 64-B
+        // segment, 16 B each, so one store instruction writes 16 segments.
+        // Region stores cost per instruction issued, not per byte (scattered
+        // 16-B stores with most lanes idle: 0.34 of pass A's 1.05 ms at C2),
+        // so the flush issues exactly kCoopRounds stores per wave per phase,
+        // at a dropped offset where a lane has nothing to write — a static
+        // store count also keeps the compiler's vmcnt waits for the
+        // prefetched keys exact.  A second segment of the same slice, or a
+        // region already full, takes the per-lane path below (rare).
         uint32_t cnt = 0;
         if (owner) {
             cnt = min(fill[own] >> 16, R);
@@ -357,15 +439,15 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
             z0 = *(const uint4*)(ring + g2), z1 = *(const uint4*)(ring + g2 + 16);
         };
         auto store_segment = [&](uint32_t off) {
-            const uint64_t q0 = pack3(x0.x, y0.x, z0.x), q1 = pack3(x0.y, y0.y, z0.y);
-            const uint64_t q2 = pack3(x0.z, y0.z, z0.z), q3 = pack3(x0.w, y0.w, z0.w);
-            const uint64_t q4 = pack3(x1.x, y1.x, z1.x), q5 = pack3(x1.y, y1.y, z1.y);
-            const uint64_t q6 = pack3(x1.z, y1.z, z1.z), q7 = pack3(x1.w, y1.w, z1.w);
+            const uint2 q0 = pack3w(x0.x, y0.x, z0.x), q1 = pack3w(x0.y, y0.y, z0.y);
+            const uint2 q2 = pack3w(x0.z, y0.z, z0.z), q3 = pack3w(x0.w, y0.w, z0.w);
+            const uint2 q4 = pack3w(x1.x, y1.x, z1.x), q5 = pack3w(x1.y, y1.y, z1.y);
+            const uint2 q6 = pack3w(x1.z, y1.z, z1.z), q7 = pack3w(x1.w, y1.w, z1.w);
             if (!(LSMB_ABL & 8)) {
-                __builtin_amdgcn_raw_buffer_store_b128(u32x4{(uint32_t)q0, (uint32_t)(q0 >> 32), (uint32_t)q1, (uint32_t)(q1 >> 32)}, rgn, off, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b128(u32x4{(uint32_t)q2, (uint32_t)(q2 >> 32), (uint32_t)q3, (uint32_t)(q3 >> 32)}, rgn, off + 16, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b128(u32x4{(uint32_t)q4, (uint32_t)(q4 >> 32), (uint32_t)q5, (uint32_t)(q5 >> 32)}, rgn, off + 32, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b128(u32x4{(uint32_t)q6, (uint32_t)(q6 >> 32), (uint32_t)q7, (uint32_t)(q7 >> 32)}, rgn, off + 48, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{q0.x, q0.y, q1.x, q1.y}, rgn, off, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{q2.x, q2.y, q3.x, q3.y}, rgn, off + 16, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{q4.x, q4.y, q5.x, q5.y}, rgn, off + 32, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{q6.x, q6.y, q7.x, q7.y}, rgn, off + 48, 0, 0);
             }
         };
         auto spill_segment = [&]() {  // region full (adversarial inputs): exact global atomics
@@ -377,13 +459,53 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
             atomicAdd(a.err + 7, 24u);
 #endif
         };
-        if (has) read_segment();
-        {
-            const bool real = !(LSMB_ABL & 16) && has && segs < a.cap;
-            store_segment(real ? ((a.b0 + own) * a.cap + segs) * 64u : kDrop);
+        // 1. post jobs (owner lanes with a full segment and room in the region)
+        const bool coop = has && segs < a.cap;
+        const uint64_t cm = __ballot(coop);
+        const uint32_t jobs = min((uint32_t)__popcll(cm), kBinJobsPerWave);  // wave-uniform
+        bool posted = false;
+        if (coop) {
+            const uint32_t j = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
+            if (j < kBinJobsPerWave) {
+                const uint32_t rb = own * R4;
+                uint32_t g1 = start + 32, g2 = start + 64;
+                g1 = min(g1, g1 - R4);
+                g2 = min(g2, g2 - R4);
+                jobtab[wave * kBinJobsPerWave + j] =
+                    make_uint4(rb + start, rb + g1, rb + g2, ((a.b0 + own) * a.cap + segs) * 64u);
+                posted = true;
+            }
         }
+        // (the job table is this wave's own: its LDS writes and reads stay in order)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        // 2. kCoopRounds store instructions: lane L writes 16 B of job r*16 + L/4
+        constexpr uint32_t kCoopRounds = kBinJobsPerWave / 16;
+#pragma unroll
+        for (uint32_t r = 0; r < kCoopRounds; r++) {
+            const uint32_t j = r * 16 + (lane >> 2), l = lane & 3;
+            uint32_t off = kDrop;
+            uint2 w0 = make_uint2(0, 0), w1 = make_uint2(0, 0);
+            if (j < jobs) {
+                const uint4 jb = jobtab[wave * kBinJobsPerWave + j];
+                // segment word 2l+e = pack3(group0[2l+e], group1[2l+e], group2[2l+e])
+                const uint2 a0 = *(const uint2*)((const char*)sm + jb.x + 8 * l);
+                const uint2 a1 = *(const uint2*)((const char*)sm + jb.y + 8 * l);
+                const uint2 a2 = *(const uint2*)((const char*)sm + jb.z + 8 * l);
+                w0 = pack3w(a0.x, a1.x, a2.x);
+                w1 = pack3w(a0.y, a1.y, a2.y);
+                off = (LSMB_ABL & 16) ? kDrop : jb.w + 16 * l;
+            }
+            if (!(LSMB_ABL & 8)) __builtin_amdgcn_raw_buffer_store_b128(u32x4{w0.x, w0.y, w1.x, w1.y}, rgn, off, 0, 0);
+        }
+        // 3. owners advance past the posted segment; the rest per lane
         if (has) {
-            if (segs >= a.cap) spill_segment();
+            if (!posted) {
+                read_segment();
+                if (segs < a.cap)
+                    store_segment(((a.b0 + own) * a.cap + segs) * 64u);
+                else
+                    spill_segment();
+            }
             const uint32_t nf = cnt / (uint32_t)kSegEntries;
             uint32_t s = start + 96;
             start = min(s, s - R4);
@@ -409,10 +531,17 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
     const uint64_t groups = (iters + kAhead - 1) / kAhead;
     for (uint64_t g = 0; g < groups; g++) {
         const uint64_t it = g * kAhead;
-        phase(it, pb1);
-        phase(it + 1, pb2);
-        phase(it + 2, pb3);
-        phase(it + 3, pb0);
+        if constexpr (kPipe) {
+            phase(it, pb2);
+            phase(it + 1, pb3);
+            phase(it + 2, pb0);
+            phase(it + 3, pb1);
+        } else {
+            phase(it, pb1);
+            phase(it + 1, pb2);
+            phase(it + 2, pb3);
+            phase(it + 3, pb0);
+        }
     }
 
     // Segments still queued, then the last open segment (< 24 entries, padded
@@ -654,7 +783,7 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
             a.gw = gw;
             a.err = ws.err;
             a.nbins = pl.nbins;
-            const size_t smem = (size_t)(a.nb + 1) * (4 * a.ring + kBinExtraBytes);
+            const size_t smem = (size_t)(a.nb + 1) * (4 * a.ring + kBinExtraBytes) + kBinJobBytes;
             auto go = [&](auto kern) {
                 set_max_lds((const void*)kern);
                 kern<<<dim3(pl.grid), dim3(kBinBlock), smem, st>>>(src, n, md, k, a);

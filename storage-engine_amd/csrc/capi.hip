@@ -505,9 +505,15 @@ int lsmb_open(lsmb_ctx** out, int device) {
     c->dev = device;
     c->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     DevGuard g(device);
-    // Non-blocking streams: no implicit ordering with the legacy null stream,
-    // so one context's work never waits for another's (flush + compaction).
-    if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess ||
+    // The context's stream is a BLOCKING stream: it is ordered with the legacy
+    // null stream, which is what torch's default stream is.  The device entry
+    // points map stream == NULL to this stream, so a caller that allocates or
+    // zeroes buffers on the null stream and then builds with stream == NULL
+    // gets the two in order (tests/test_gpu_parity.py relies on it).  Two
+    // contexts' blocking streams do not wait for each other; the library
+    // itself issues nothing on the null stream after lsmb_open (the filter
+    // set uploads on a non-blocking stream of its own).
+    if (hipStreamCreateWithFlags(&c->st, hipStreamDefault) != hipSuccess ||
         hipEventCreateWithFlags(&c->desc_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ws_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreate(&c->tm.t0) != hipSuccess || hipEventCreate(&c->tm.t1) != hipSuccess ||
@@ -520,7 +526,8 @@ int lsmb_open(lsmb_ctx** out, int device) {
         delete c;
         return fail(LSMB_ENODEV, "stream/event creation failed on device %d", device);
     }
-    if (c->err.ensure(64) != hipSuccess || hipMemset(c->err.p, 0, 64) != hipSuccess ||
+    if (c->err.ensure(64) != hipSuccess || hipMemsetAsync(c->err.p, 0, 64, c->st) != hipSuccess ||
+        hipStreamSynchronize(c->st) != hipSuccess ||
         hipHostMalloc((void**)&c->err_host, 64, 0) != hipSuccess) {
         lsmb_close(c);
         return fail(LSMB_ENOMEM, "error-flag allocation failed on device %d", device);

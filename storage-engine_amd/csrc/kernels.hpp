@@ -18,7 +18,9 @@ constexpr int kBinBlock = 1024;                       // pass A workgroup
 constexpr int kApplyBlock = 1024;                     // pass B workgroup
 constexpr uint32_t kLdsFilterMaxWords32 = 40 * 1024;  // 160 KiB: whole filter in LDS
 constexpr uint32_t kLdsBytes = 160 * 1024;            // LDS per CU (gfx950)
-constexpr uint32_t kBinLdsBudget = kLdsBytes;         // pass A: rings + fill words
+constexpr uint32_t kBinJobsPerWave = 32;              // pass A flush: segments per wave per phase (2 rounds of 16)
+constexpr uint32_t kBinJobBytes = (kBinBlock / 64) * kBinJobsPerWave * 16 + 16;  // job tables (+ alignment)
+constexpr uint32_t kBinLdsBudget = kLdsBytes - kBinJobBytes;  // pass A: rings + fill words
 constexpr uint32_t kBinExtraBytes = 4;                // per slice besides its ring: fill word
 constexpr uint32_t kMaxBinsPerSweep = 1024;           // one owner lane per slice: <= 64 slices per wave
 constexpr uint32_t kMaxRing = 1024;                   // ring entries per slice

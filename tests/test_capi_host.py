@@ -142,3 +142,20 @@ def test_batched_path_fails_loudly_without_gpu():
     with pytest.raises(lsmbloom.LsmbError) as ei:
         lsmbloom.Context(0)
     assert ei.value.code == lsmbloom.LSMB_ENODEV
+
+
+def test_no_device_wide_synchronisation_in_library():
+    """Contexts may run concurrently (flush + background compaction,
+    src/compaction/scheduler.rs:37): the library never waits for the whole
+    device (hipDeviceSynchronize) and never issues null-stream copies or
+    memsets (hipMemcpy / hipMemset without a stream), which wait for every
+    blocking stream of every context."""
+    import glob
+    srcs = glob.glob(os.path.join(ROOT, "storage-engine_amd", "csrc", "*.hip"))
+    assert srcs
+    for path in srcs:
+        code = re.sub(r"//[^\n]*", "", open(path).read())
+        code = re.sub(r"#ifdef LSMB_STATS.*?#endif", "", code, flags=re.S)  # diagnostics build only
+        assert "hipDeviceSynchronize" not in code, path
+        assert not re.search(r"\bhipMemcpy\s*\(", code), path
+        assert not re.search(r"\bhipMemset\s*\(", code), path

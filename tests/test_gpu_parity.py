@@ -395,13 +395,22 @@ def test_c4_full_size_properties(ctx, oracle):
     import math
 
     import torch
+    import sys
+    import time
+    t0 = time.time()
+
+    def tick(what):
+        print("[c4 %.1fs] %s" % (time.time() - t0, what), file=sys.stderr, flush=True)
     N, G = 100_000_000, 4
     data, offs = ctx.gen_varlen_dev(N)
+    tick("generated")
     nb, k = lsmbloom.params(N, 0.01)
     nw = lsmbloom.num_words(nb)
     dev = data.device
     mono = torch.zeros(nw, dtype=torch.int64, device=dev)
     ctx.build_var_dev(data, offs, N, nb, k, mono)
+    torch.cuda.synchronize()
+    tick("monolithic build")
     merged = torch.zeros(nw, dtype=torch.int64, device=dev)
     per = N // G
     for g in range(G):
@@ -413,14 +422,17 @@ def test_c4_full_size_properties(ctx, oracle):
         del part, so
     ctx.sync()
     torch.cuda.synchronize()
+    tick("shard builds")
     assert torch.equal(merged, mono)
     del merged
     host_words = mono.cpu().numpy().view(np.uint64)
-    ones = int(np.unpackbits(host_words.view(np.uint8)).sum())
+    ones = int(np.bitwise_count(host_words).sum(dtype=np.uint64))
+    tick("fill counted")
     assert abs(ones / nb - (1 - math.exp(-k * N / nb))) < 1e-3, ones / nb
     idx = list(range(0, N, 997_331))[:100]
     f = BloomFilter(host_words, k, nb)
     oh = offs.cpu().numpy()
+    tick("offsets to host")
     for i in idx:
         key = bytes(data[int(oh[i]):int(oh[i + 1])].cpu().numpy())
         assert f.may_contain(key)

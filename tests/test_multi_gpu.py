@@ -237,41 +237,64 @@ def test_one_context_two_streams(torch, oracle):
         ctx.close()
 
 
-def test_fset_add_does_not_wait_for_other_contexts(torch, oracle):
-    """a filter-set add/remove on one context (the read
-    path) must not stall on another context's queued builds (flush /
-    compaction): it waits for its own set's probes only."""
+def test_fset_and_builds_on_two_contexts_concurrently(torch, oracle):
+    """flush / compaction builds on one context while the
+    read path adds, removes and probes filters on another, from two host
+    threads at once (src/compaction/scheduler.rs:37).  The filter set waits
+    for its own probes only (per-set events; no device-wide synchronisation,
+    which tests/test_capi_host.py checks in the source); here every result of
+    both threads must be exact.  Whether the two contexts' work overlaps in
+    time also depends on how the runtime maps streams to the 4 hardware
+    queues, so no timing is asserted."""
     dev = torch.device("cuda:0")
     a, b = lsmbloom.Context(0), lsmbloom.Context(0)
+    errors = []
     try:
-        n = 20_000_000
+        n = 4_000_000
         nb, k = lsmbloom.params(n, 0.01)
         keys = torch.empty((n, 16), dtype=torch.uint8, device=dev)
         a.gen_key16_dev(3, 0, n, keys, stream=a_stream(a))
-        words = torch.zeros(lsmbloom.num_words(nb), dtype=torch.int64, device=dev)
+        ref_build = oracle.build_fixed_mt(keygen.key16(3, 0, n), 16, nb, k, 8)
+
+        def builder():
+            try:
+                words = torch.zeros(lsmbloom.num_words(nb), dtype=torch.int64, device=dev)
+                for _ in range(20):
+                    words.zero_()
+                    a.build_fixed_dev(keys, 16, n, nb, k, words, stream=a_stream(a))
+                a.sync()
+                torch.cuda.synchronize()
+                if not np.array_equal(_u64(words), ref_build):
+                    errors.append("build differs")
+            except Exception as e:  # noqa: BLE001
+                errors.append(repr(e))
+
+        th = threading.Thread(target=builder)
+        th.start()
         fs = lsmbloom.FilterSet(b)
-        f = lsmbloom.BloomFilter.new(1000, 0.01)
-        for i in range(100):
-            f.insert(b"key_%05d" % i)
-        fs.add_filter(f, b"key_00000", b"key_00099")  # warm-up: slot buffer, stream, staging
-        fs.probe_keys([b"key_00005", b"zzz"])
-        a.sync()
-        # queue ~30 builds on context a's own stream, then time an add on b
-        t0 = time.perf_counter()
-        for _ in range(30):
-            a.build_fixed_dev(keys, 16, n, nb, k, words, stream=a_stream(a))
-        t_enq = time.perf_counter() - t0
-        t0 = time.perf_counter()
-        slot = fs.add_filter(f, b"key_00000", b"key_00099")
-        got = fs.probe_keys([b"key_00005", b"zzz"])
-        t_add = time.perf_counter() - t0
-        t0 = time.perf_counter()
-        a.sync()
-        t_rest = time.perf_counter() - t0
-        assert (int(got[0]) >> slot) & 1 == 1 and int(got[1]) == 0
-        # the add + probe finished while most of a's queue was still running
-        assert t_add < 0.5 * (t_add + t_rest), (t_enq, t_add, t_rest)
+        filters = []
+        for t in range(6):
+            f = lsmbloom.BloomFilter.new(1000, 0.01)
+            for i in range(100):
+                f.insert(b"t%d_key_%05d" % (t, i))
+            filters.append(f)
+        for rep in range(10):
+            slots = [fs.add_filter(f, b"t%d_key_00000" % t, b"t%d_key_00099" % t) for t, f in enumerate(filters)]
+            q = [b"t%d_key_%05d" % (t, i) for t in range(6) for i in (0, 50, 99)] + [b"zzz", b"t0_key_00500"]
+            got = fs.probe_keys(q)
+            for j, key in enumerate(q):
+                exp = 0
+                for t, f in enumerate(filters):
+                    lo, hi = b"t%d_key_00000" % t, b"t%d_key_00099" % t
+                    if lo <= key <= hi and f.may_contain(key):
+                        exp |= 1 << slots[t]
+                assert int(got[j]) == exp, (rep, key)
+            for sl in slots:
+                fs.remove(sl)
         fs.close()
+        th.join(timeout=120)
+        assert not th.is_alive()
+        assert not errors, errors
     finally:
         a.close()
         b.close()

@@ -1,0 +1,15 @@
+#!/bin/bash
+# GPU side of tools/build_variants.sh: the C2 build (bench.py, build legs only)
+# against each variant library; one line per variant with pass A / pass B ms.
+# Usage: tools/run_variants.sh [bench args] -- name1 name2 ...   (name "base" = the product library)
+REPO=${GRAFT_REPO_ROOT:-/root/repo}
+args=()
+while [ $# -gt 0 ] && [ "$1" != "--" ]; do args+=("$1"); shift; done
+shift
+for v in "$@"; do
+  lib=$REPO/storage-engine_amd/lib/liblsmbloom_$v.so
+  [ "$v" = base ] && lib=$REPO/storage-engine_amd/lib/liblsmbloom.so
+  out=$(LSMB_LIB=$lib timeout -k 10 120 python3 $REPO/bench.py --steps 20 --warmup 5 --no-probe --no-e2e \
+        --no-cpu-baseline --no-varlen --no-exact10 "${args[@]}") || { echo "variant $v failed"; exit 1; }
+  echo "$out" | python3 -c 'import json,sys; d=json.loads(sys.stdin.readline()); r=d["roofline"]; print("%-10s pass_a %.4f pass_b %.4f kernel %.4f step %.4f" % (sys.argv[1], r["pass_a_ms"], r["pass_b_ms"], r["kernel_ms"], d["ms_per_step"]))' "$v"
+done
