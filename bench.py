@@ -487,6 +487,19 @@ def bench_e2e(ctx, keys, n, nb, k, reps=3):
                       "bit_exact": bool(np.array_equal(np.frombuffer(blk[12:].tobytes(), dtype=np.uint64), ref)
                                         and np.array_equal(blk, blk_gpu))})
     res["host_max_keys"] = thr
+    # Flush-shaped end to end from a host structure: a C++
+    # driver walks an ordered memtable of 4 M 16-B keys and feeds every key to
+    # lsmb_stream_add (chunks upload and build while the walk goes on), then
+    # lsmb_stream_finish_block; beside it the same walk through the library's
+    # per-key host insert + serialize (the reference's flush, one thread).
+    import subprocess
+    exe = os.path.join(ROOT, "storage-engine_amd", "build", "flush_e2e")
+    try:
+        r = subprocess.run([exe, "4000000"], capture_output=True, text=True, timeout=180)
+        res["flush_walk"] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
+            {"error": (r.stdout + r.stderr)[-300:]}
+    except Exception as e:  # report, never lose the bench line
+        res["flush_walk"] = {"error": repr(e)[:200]}
     res["sst_flush_latency"] = small
     return res
 

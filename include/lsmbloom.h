@@ -145,6 +145,42 @@ int lsmb_build_block(lsmb_ctx* ctx, const uint8_t* data, const uint64_t* offsets
                      uint64_t n, uint32_t num_bits, uint32_t num_hashes, uint8_t* block,
                      uint64_t block_len);
 
+/* ---- streaming ingestion (the flush / compaction add_key loop) ----------- */
+/* The store's flush walks the frozen memtable and adds every key
+ * (src/db/mod.rs:379-383 -> SSTableBuilder::add -> BloomFilterBuilder::add_key,
+ * src/sstable/builder.rs:93); compaction does the same over its merged
+ * entries (src/compaction/scheduler.rs:113-125,152-158).  An lsmb_stream takes
+ * those keys one at a time while the walk is still going: each add is a copy
+ * into pinned staging, and every full staging chunk (LSMB_STREAM_CHUNK_MB,
+ * default 128) is uploaded and built asynchronously while the caller keeps
+ * adding into the other chunk.  finish writes the serialized bloom block (or
+ * the words) of BloomFilter::new + insert of every added key.  A run of at
+ * most lsmb_host_max_keys() keys never touches the device (host loop at
+ * finish); with ctx == NULL the stream is host-only and finish of a larger
+ * run is LSMB_EINVAL.  One stream per thread; reusable after finish
+ * (lsmb_stream_reset for another filter size). */
+typedef struct lsmb_stream lsmb_stream;
+
+int lsmb_stream_open(lsmb_ctx* ctx, uint32_t num_bits, uint32_t num_hashes, lsmb_stream** out);
+int lsmb_stream_reset(lsmb_stream* s, uint32_t num_bits, uint32_t num_hashes);
+void lsmb_stream_close(lsmb_stream* s);
+
+/* BloomFilterBuilder::add_key (src/bloom/builder.rs:21-23): appends one key. */
+int lsmb_stream_add(lsmb_stream* s, const uint8_t* key, uint64_t key_len);
+
+/* Appends n keys: key i = data[offsets[i] .. offsets[i+1]). */
+int lsmb_stream_add_batch(lsmb_stream* s, const uint8_t* data, const uint64_t* offsets, uint64_t n);
+
+/* Keys added since open / the last finish. */
+uint64_t lsmb_stream_count(const lsmb_stream* s);
+
+/* Finishes the filter: the bytes BloomFilter::serialize returns
+ * (src/bloom/mod.rs:102-115) into block[0 .. lsmb_serialized_size(num_bits)),
+ * or the ceil(num_bits/64) words.  Synchronous; the stream then starts a new,
+ * empty filter of the same size. */
+int lsmb_stream_finish_block(lsmb_stream* s, uint8_t* block, uint64_t block_len);
+int lsmb_stream_finish_words(lsmb_stream* s, uint64_t* words);
+
 /* ---- batched probe (may_contain over a batch of keys x filters) --------- */
 /* For key i and filter f: bit (f % 8) of out_mask[i * ceil(nfilt/8) + f / 8]
  * = may_contain(filter f, key i), exactly what SSTable::get's bloom check

@@ -90,6 +90,14 @@ SIGNATURES = {
     "lsmb_multi_build_block": (ctypes.c_int, [vp, u8p, u64p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
                                               ctypes.c_uint32, u8p, ctypes.c_uint64]),
     "lsmb_multi_last_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_float)]),
+    "lsmb_stream_open": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(vp)]),
+    "lsmb_stream_reset": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32]),
+    "lsmb_stream_close": (None, [vp]),
+    "lsmb_stream_add": (ctypes.c_int, [vp, u8p, ctypes.c_uint64]),
+    "lsmb_stream_add_batch": (ctypes.c_int, [vp, u8p, u64p, ctypes.c_uint64]),
+    "lsmb_stream_count": (ctypes.c_uint64, [vp]),
+    "lsmb_stream_finish_block": (ctypes.c_int, [vp, u8p, ctypes.c_uint64]),
+    "lsmb_stream_finish_words": (ctypes.c_int, [vp, u64p]),
     "lsmb_last_build_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_float)]),
     "lsmb_set_timing": (ctypes.c_int, [vp, ctypes.c_int]),
 }
@@ -324,6 +332,59 @@ class Context:
         a = (ctypes.c_float * 3)()
         _check(lib().lsmb_last_build_ms(self.h, a))
         return tuple(a)
+
+
+class KeyStream:
+    """Streaming ingestion (lsmb_stream): the flush's add_key loop
+    (src/db/mod.rs:379-383 -> SSTableBuilder::add -> BloomFilterBuilder::add_key)
+    with full staging chunks uploaded and built while keys keep arriving.
+    finish_block() == BloomFilter::new(..) + inserts, serialized."""
+
+    def __init__(self, ctx, num_bits, k):
+        """ctx None: host-only (runs of at most host_max_keys() keys)."""
+        h = vp()
+        _check(lib().lsmb_stream_open(ctx.h if ctx else None, num_bits, k, ctypes.byref(h)))
+        self.h, self.ctx, self.num_bits, self.k = h, ctx, num_bits, k
+
+    def close(self):
+        if self.h:
+            lib().lsmb_stream_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self, num_bits, k):
+        _check(lib().lsmb_stream_reset(self.h, num_bits, k))
+        self.num_bits, self.k = num_bits, k
+
+    def add(self, key):
+        a, n = _key(key)
+        _check(lib().lsmb_stream_add(self.h, _p(a, u8p), n))
+
+    def add_batch(self, data, offsets):
+        data = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        if data.size == 0:
+            data = np.zeros(1, np.uint8)
+        _check(lib().lsmb_stream_add_batch(self.h, _p(data, u8p), _p(offsets, u64p), offsets.size - 1))
+
+    def count(self):
+        return int(lib().lsmb_stream_count(self.h))
+
+    def finish_block(self, out=None):
+        if out is None:
+            out = np.empty(serialized_size(self.num_bits), dtype=np.uint8)
+        _check(lib().lsmb_stream_finish_block(self.h, _p(out, u8p), out.size))
+        return out
+
+    def finish_words(self):
+        w = np.zeros(max(num_words(self.num_bits), 1), dtype=np.uint64)
+        _check(lib().lsmb_stream_finish_words(self.h, _p(w, u64p)))
+        return w[: num_words(self.num_bits)]
 
 
 class FilterSet:

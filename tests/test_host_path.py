@@ -106,3 +106,31 @@ def test_host_path_or_accumulates(oracle, threshold):
                                     lsmbloom._p(w, lsmbloom.u64p)) == 0
     ref = oracle.build_fixed(b, 16, nb, k, words=oracle.build_fixed(a, 16, nb, k))
     assert np.array_equal(w, ref)
+
+
+def test_stream_host_only_flush_loop(oracle, threshold):
+    """lsmb_stream without a device context: the flush's add_key loop over a
+    memtable-sized run (src/db/mod.rs:379-383, SSTableBuilder::new sizing)
+    finishes on the host; a run past the threshold is refused, not built on
+    the CPU."""
+    nb, k = lsmbloom.params(1000, 0.01)
+    st = lsmbloom.KeyStream(None, nb, k)
+    memtable = sorted({b"key_%05d" % i: b"v" for i in range(1000)}.items())  # frozen.iter() order
+    for key, _value in memtable:
+        st.add(key)
+    assert st.count() == 1000
+    blk = st.finish_block()
+    data, offs = keygen.pack([kv[0] for kv in memtable])
+    assert bytes(blk) == bytes(oracle.serialize(oracle.build_var(data, offs, nb, k), nb, k))
+    # the stream restarts empty: a second run of other keys
+    for i in range(10):
+        st.add(b"other_%d" % i)
+    w = st.finish_words()
+    d2, o2 = keygen.pack([b"other_%d" % i for i in range(10)])
+    assert np.array_equal(w, oracle.build_var(d2, o2, nb, k))
+    lsmbloom.set_host_max_keys(5)
+    for i in range(6):
+        st.add(b"k%d" % i)
+    with pytest.raises(ValueError):
+        st.finish_block()
+    st.close()
