@@ -176,51 +176,83 @@ __device__ __forceinline__ Pfx16 prefix16(const uint8_t* p, uint64_t len) {
     return r;
 }
 
-__device__ __forceinline__ int cmp_pfx(const Pfx16& k, const uint8_t* kp, uint64_t kl, const Pfx16& b,
-                                       const uint8_t* bp, uint32_t bl) {
-    if (k.w0 != b.w0) return k.w0 < b.w0 ? -1 : 1;
-    if (k.w1 != b.w1) return k.w1 < b.w1 ? -1 : 1;
-    if (kl <= 16 && bl <= 16) return kl < bl ? -1 : (kl > bl ? 1 : 0);
-    return key_cmp(kp, kl, bp, bl);
+// Per workgroup: the set's boundary points and region masks into LDS.
+struct FsetLds {
+    uint64_t w0[kFsetMaxPoints], w1[kFsetMaxPoints];
+    const uint8_t* p[kFsetMaxPoints];
+    uint32_t len[kFsetMaxPoints];
+    uint64_t regmask[2 * kFsetMaxPoints + 1];
+};
+
+__device__ __forceinline__ void stage_ranges(const FsetRanges& rg, FsetLds& L) {
+    for (uint32_t j = threadIdx.x; j < rg.npts; j += blockDim.x) {
+        const FsetPoint q = rg.pts[j];
+        L.w0[j] = q.w0;
+        L.w1[j] = q.w1;
+        L.p[j] = q.p;
+        L.len[j] = q.len;
+    }
+    for (uint32_t j = threadIdx.x; j < 2 * rg.npts + 1; j += blockDim.x) L.regmask[j] = rg.regmask[j];
 }
 
-// Per workgroup: every descriptor's lo/hi prefixes into LDS.
-__device__ __forceinline__ void stage_bounds(const RangedFilter* fl, uint32_t nfilt, Pfx16* blo, Pfx16* bhi) {
-    for (uint32_t f = threadIdx.x; f < nfilt; f += blockDim.x) {
-        blo[f] = prefix16(fl[f].lo, fl[f].lo_len);
-        bhi[f] = prefix16(fl[f].hi, fl[f].hi_len);
+// The key's region among the sorted points: a branch-free binary search on
+// the 16-byte prefixes (a uniform loop of ceil(log2(npts + 1)) steps), then
+// exact compares over the run of points whose prefix equals the key's (rare:
+// keys or bounds longer than 16 bytes sharing their first 16).
+__device__ __forceinline__ uint32_t key_region(const Pfx16& kx, const uint8_t* kp, uint64_t kl, const FsetLds& L,
+                                               uint32_t m) {
+    uint32_t lo = 0;
+    for (uint32_t step = m ? 1u << (31 - __builtin_clz(m)) : 0u; step; step >>= 1) {
+        const uint32_t j = lo + step - 1;
+        if (j < m) {
+            const uint64_t a = L.w0[j], b = L.w1[j];
+            if (a < kx.w0 || (a == kx.w0 && b < kx.w1)) lo += step;
+        }
     }
+    uint32_t e = 0;
+    while (lo < m && L.w0[lo] == kx.w0 && L.w1[lo] == kx.w1) {
+        const uint32_t pl = L.len[lo];
+        const int c = (kl <= 16 && pl <= 16) ? (kl < pl ? -1 : (kl > pl ? 1 : 0)) : key_cmp(kp, kl, L.p[lo], pl);
+        if (c > 0) {
+            lo++;
+            continue;
+        }
+        e = c == 0;
+        break;
+    }
+    return 2 * lo + e;
 }
 
 // Filter-set probe (multi-get pre-check): per key, for every SSTable of the
 // set, the two checks SSTable::get makes before touching the index
 // (src/sstable/reader.rs:192-199): key inside [min_key, max_key], then
-// bloom.may_contain(key).  One hash per key; descriptors staged in LDS.
+// bloom.may_contain(key).  One hash per key; the range check of all tables
+// is one region lookup (key_region); descriptors staged in LDS.
 template <class Src>
 __global__ __launch_bounds__(256) void k_fset_probe(Src src, uint64_t n, const RangedFilter* __restrict__ filters,
-                                                    uint32_t nfilt, uint64_t* __restrict__ out) {
+                                                    uint32_t nfilt, FsetRanges rg, uint64_t* __restrict__ out) {
     __shared__ RangedFilter fl[64];
-    __shared__ Pfx16 blo[64], bhi[64];
+    __shared__ FsetLds L;
     for (uint32_t f = threadIdx.x; f < nfilt; f += blockDim.x) fl[f] = filters[f];
+    stage_ranges(rg, L);
     __syncthreads();
-    stage_bounds(fl, nfilt, blo, bhi);
-    __syncthreads();
+    const uint32_t npts = rg.npts;
     const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
         const H128 h = src.hash(i);
         const uint8_t* kp = src.bytes(i);
         const uint64_t kl = src.key_len(i);
-        const Pfx16 kx = prefix16(kp, kl);
+        uint64_t rmask = L.regmask[key_region(prefix16(kp, kl), kp, kl, L, npts)];
         uint64_t m = 0;
         // Positions of the last (num_bits, k <= 8) walked: the store's SST
         // filters all share one sizing (builder.rs:51,74), so one walk serves
         // every table in range.
         uint32_t cpos[8];
         uint32_t cnb = 0, ck = 0;
-        for (uint32_t f = 0; f < nfilt; f++) {
+        while (rmask) {
+            const uint32_t f = (uint32_t)__builtin_ctzll(rmask);
+            rmask &= rmask - 1;
             const RangedFilter& R = fl[f];
-            if (cmp_pfx(kx, kp, kl, blo[f], R.lo, R.lo_len) < 0 || cmp_pfx(kx, kp, kl, bhi[f], R.hi, R.hi_len) > 0)
-                continue;
             bool hit = true;
             if (R.f.k && R.f.k <= 8) {
                 if (R.f.num_bits != cnb || R.f.k != ck) {
@@ -258,18 +290,20 @@ __global__ __launch_bounds__(256) void k_fset_probe(Src src, uint64_t n, const R
 // Filter-set probe when every filter of the set shares (num_bits, k) and the
 // bit-sliced table fits LDS (the store's SST filters: new(1000, 0.01), 9 568
 // bits, k = 7): entry p of the table holds the set's bit p, one bit per
-// descriptor.  A key pays the range checks, then k LDS reads ANDed over all
-// in-range filters at once (bits read from L2 per filter in k_fset_probe).
+// descriptor.  A key pays one region lookup for the range checks, then k LDS
+// reads ANDed over all in-range filters at once (bits read from L2 per
+// filter in k_fset_probe).
 template <class Src, typename T, int K>
 __global__ __launch_bounds__(256) void k_fset_sliced(Src src, uint64_t n, const RangedFilter* __restrict__ filters,
-                                                     uint32_t nfilt, uint32_t k_, uint64_t* __restrict__ out) {
+                                                     uint32_t nfilt, FsetRanges rg, uint32_t k_,
+                                                     uint64_t* __restrict__ out) {
     extern __shared__ __align__(16) uint8_t smem_raw[];
     __shared__ RangedFilter fl[64];
-    __shared__ Pfx16 blo[64], bhi[64];
+    __shared__ FsetLds L;
     T* table = reinterpret_cast<T*>(smem_raw);
     for (uint32_t f = threadIdx.x; f < nfilt; f += blockDim.x) fl[f] = filters[f];
+    stage_ranges(rg, L);
     __syncthreads();
-    stage_bounds(fl, nfilt, blo, bhi);
     const uint32_t num_bits = fl[0].f.num_bits;
     const Mod32 md = fl[0].f.md;
     bool ident = true;  // slots 0..nfilt-1 all live: table bit f is output bit f
@@ -288,18 +322,13 @@ __global__ __launch_bounds__(256) void k_fset_sliced(Src src, uint64_t n, const 
         for (int b = 0; b < 32; b++) table[w * 32 + b] = acc[b];
     }
     __syncthreads();
+    const uint32_t npts = rg.npts;
     const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
         const H128 h = src.hash(i);
         const uint8_t* kp = src.bytes(i);
         const uint64_t kl = src.key_len(i);
-        const Pfx16 kx = prefix16(kp, kl);
-        T m = 0;
-        for (uint32_t f = 0; f < nfilt; f++) {
-            const RangedFilter& R = fl[f];
-            if (cmp_pfx(kx, kp, kl, blo[f], R.lo, R.lo_len) >= 0 && cmp_pfx(kx, kp, kl, bhi[f], R.hi, R.hi_len) <= 0)
-                m |= (T)((T)1 << f);
-        }
+        T m = (T)L.regmask[key_region(prefix16(kp, kl), kp, kl, L, npts)];
         if (m) {
             Walk32 pw(md, h.lo, h.hi);
             if (K > 0) {
@@ -326,8 +355,8 @@ __global__ __launch_bounds__(256) void k_fset_sliced(Src src, uint64_t n, const 
 }
 
 template <class Src>
-hipError_t fset_probe_with(const Src& src, uint64_t n, const RangedFilter* df, uint32_t nfilt, uint32_t shared_nb,
-                           uint32_t shared_k, uint64_t* out, int num_cus, hipStream_t st) {
+hipError_t fset_probe_with(const Src& src, uint64_t n, const RangedFilter* df, uint32_t nfilt, const FsetRanges& rg,
+                           uint32_t shared_nb, uint32_t shared_k, uint64_t* out, int num_cus, hipStream_t st) {
     uint64_t g = (n + 255) / 256;
     const uint64_t gmax = (uint64_t)num_cus * 8;
     if (g > gmax) g = gmax;
@@ -338,7 +367,7 @@ hipError_t fset_probe_with(const Src& src, uint64_t n, const RangedFilter* df, u
         if (smem <= 64 * 1024) {
             auto go = [&](auto kern) {
                 hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-                kern<<<dim3((uint32_t)g), dim3(256), smem, st>>>(src, n, df, nfilt, shared_k, out);
+                kern<<<dim3((uint32_t)g), dim3(256), smem, st>>>(src, n, df, nfilt, rg, shared_k, out);
             };
             if (tsz == 1) {
                 if (shared_k == 7) go(k_fset_sliced<Src, uint8_t, 7>);
@@ -349,7 +378,7 @@ hipError_t fset_probe_with(const Src& src, uint64_t n, const RangedFilter* df, u
             return hipGetLastError();
         }
     }
-    k_fset_probe<Src><<<dim3((uint32_t)g), dim3(256), 0, st>>>(src, n, df, nfilt, out);
+    k_fset_probe<Src><<<dim3((uint32_t)g), dim3(256), 0, st>>>(src, n, df, nfilt, rg, out);
     return hipGetLastError();
 }
 
@@ -396,14 +425,16 @@ hipError_t probe_with(const Src& src, uint64_t n, const ProbeFilter* hf, uint32_
 
 }  // namespace
 
-hipError_t launch_fset_probe(const KeyBatch& kb, const RangedFilter* df, uint32_t nfilt, uint32_t shared_nb,
-                             uint32_t shared_k, uint64_t* out, int num_cus, hipStream_t st) {
+hipError_t launch_fset_probe(const KeyBatch& kb, const RangedFilter* df, uint32_t nfilt, const FsetRanges& rg,
+                             uint32_t shared_nb, uint32_t shared_k, uint64_t* out, int num_cus, hipStream_t st) {
     if (kb.n == 0) return hipSuccess;
-    if (nfilt > 64) return hipErrorInvalidValue;
-    if (kb.offsets) return fset_probe_with(VarLen{kb.data, kb.offsets}, kb.n, df, nfilt, shared_nb, shared_k, out, num_cus, st);
+    if (nfilt > 64 || rg.npts > kFsetMaxPoints) return hipErrorInvalidValue;
+    if (kb.offsets)
+        return fset_probe_with(VarLen{kb.data, kb.offsets}, kb.n, df, nfilt, rg, shared_nb, shared_k, out, num_cus, st);
     if (kb.key_len == 16 && (reinterpret_cast<uintptr_t>(kb.data) & 15) == 0)
-        return fset_probe_with(Fixed16{reinterpret_cast<const uint4*>(kb.data)}, kb.n, df, nfilt, shared_nb, shared_k, out, num_cus, st);
-    return fset_probe_with(FixedN{kb.data, kb.key_len}, kb.n, df, nfilt, shared_nb, shared_k, out, num_cus, st);
+        return fset_probe_with(Fixed16{reinterpret_cast<const uint4*>(kb.data)}, kb.n, df, nfilt, rg, shared_nb,
+                               shared_k, out, num_cus, st);
+    return fset_probe_with(FixedN{kb.data, kb.key_len}, kb.n, df, nfilt, rg, shared_nb, shared_k, out, num_cus, st);
 }
 
 hipError_t launch_probe(const KeyBatch& kb, const ProbeFilter* hf, uint32_t nfilt,

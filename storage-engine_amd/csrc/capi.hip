@@ -842,8 +842,10 @@ struct lsmb_fset {
         std::vector<uint8_t> lo, hi;
     };
     Slot slot[64];
-    DevBuf ranges;  // every live slot's lo and hi keys
+    DevBuf ranges;  // the distinct boundary keys' bytes
+    DevBuf points;  // FsetPoint[npts] then regmask[2 * npts + 1]
     DevBuf desc;    // RangedFilter[ndesc]
+    FsetRanges rg{};
     uint32_t ndesc = 0;
     uint32_t shared_nb = 0, shared_k = 0;  // (num_bits, k) of every live slot, or 0 when they differ
     bool dirty = true;
@@ -876,18 +878,43 @@ int fset_note_probe(lsmb_fset* fs, hipStream_t st) {
     return LSMB_OK;
 }
 
-// Rebuilds the device descriptors after an add/remove (rare; probes re-use them).
+// Rebuilds the device descriptors after an add/remove (rare; probes re-use
+// them): the descriptors, and the sorted boundary points of the live tables'
+// key ranges with one in-range mask per region (FsetRanges, kernels.hpp).
 int fset_refresh(lsmb_fset* fs) {
     if (!fs->dirty) return LSMB_OK;
+    std::vector<const lsmb_fset::Slot*> live;
+    std::vector<uint32_t> slot_of;
+    for (uint32_t s = 0; s < 64; s++)
+        if (fs->slot[s].live) {
+            live.push_back(&fs->slot[s]);
+            slot_of.push_back(s);
+        }
+    // distinct bounds, sorted as Rust's [u8] Ord (std::vector<uint8_t> < is
+    // the same unsigned lexicographic order, a proper prefix first)
+    std::vector<std::vector<uint8_t>> pts;
+    for (const auto* S : live) {
+        pts.push_back(S->lo);
+        pts.push_back(S->hi);
+    }
+    std::sort(pts.begin(), pts.end());
+    pts.erase(std::unique(pts.begin(), pts.end()), pts.end());
+    const uint32_t m = (uint32_t)pts.size();
+    // region masks over descriptor indices: region 2r = (P[r-1], P[r]),
+    // region 2r+1 = {P[r]}
+    std::vector<uint64_t> regmask(2 * m + 1, 0);
+    for (uint32_t d = 0; d < live.size(); d++) {
+        const auto* S = live[d];
+        if (S->hi < S->lo) continue;  // an empty range holds no key
+        const uint32_t a = (uint32_t)(std::lower_bound(pts.begin(), pts.end(), S->lo) - pts.begin());
+        const uint32_t b = (uint32_t)(std::lower_bound(pts.begin(), pts.end(), S->hi) - pts.begin());
+        for (uint32_t reg = 2 * a + 1; reg <= 2 * b + 1; reg++) regmask[reg] |= 1ull << d;
+    }
     std::vector<uint8_t> blob;
-    std::vector<RangedFilter> d;
-    std::vector<std::pair<uint64_t, uint64_t>> at;  // blob offsets of lo, hi
-    for (uint32_t s = 0; s < 64; s++) {
-        const auto& S = fs->slot[s];
-        if (!S.live) continue;
-        at.push_back({blob.size(), blob.size() + S.lo.size()});
-        blob.insert(blob.end(), S.lo.begin(), S.lo.end());
-        blob.insert(blob.end(), S.hi.begin(), S.hi.end());
+    std::vector<uint64_t> at;
+    for (const auto& p : pts) {
+        at.push_back(blob.size());
+        blob.insert(blob.end(), p.begin(), p.end());
     }
     if (int rc = fset_wait_probes(fs)) return rc;  // no probe may still read the old descriptors
     // grow geometrically from 4 KiB: a re-allocation frees the old buffer, and
@@ -897,29 +924,47 @@ int fset_refresh(lsmb_fset* fs) {
     HIP_TRY(fs->ranges.ensure(want));
     if (!blob.empty()) HIP_TRY(hipMemcpyAsync(fs->ranges.p, blob.data(), blob.size(), hipMemcpyHostToDevice, fs->ust));
     const uint8_t* rb = (const uint8_t*)fs->ranges.p;
-    uint32_t j = 0;
-    for (uint32_t s = 0; s < 64; s++) {
-        const auto& S = fs->slot[s];
-        if (!S.live) continue;
+    std::vector<uint8_t> pbuf(sizeof(FsetPoint) * kFsetMaxPoints + 8 * (2 * kFsetMaxPoints + 1));
+    FsetPoint* fp = (FsetPoint*)pbuf.data();
+    for (uint32_t j = 0; j < m; j++) {
+        const auto& p = pts[j];
+        uint8_t pad[16] = {0};
+        memcpy(pad, p.data(), std::min<size_t>(16, p.size()));
+        uint64_t w0 = 0, w1 = 0;
+        for (int b = 0; b < 8; b++) {
+            w0 = (w0 << 8) | pad[b];
+            w1 = (w1 << 8) | pad[8 + b];
+        }
+        fp[j].w0 = w0;
+        fp[j].w1 = w1;
+        fp[j].p = rb + at[j];
+        fp[j].len = (uint32_t)p.size();
+        fp[j].pad = 0;
+    }
+    memcpy(pbuf.data() + sizeof(FsetPoint) * m, regmask.data(), 8 * regmask.size());
+    HIP_TRY(fs->points.ensure(pbuf.size()));
+    HIP_TRY(hipMemcpyAsync(fs->points.p, pbuf.data(), sizeof(FsetPoint) * m + 8 * regmask.size(), hipMemcpyHostToDevice,
+                           fs->ust));
+    fs->rg.pts = (const FsetPoint*)fs->points.p;
+    fs->rg.regmask = (const uint64_t*)((const uint8_t*)fs->points.p + sizeof(FsetPoint) * m);
+    fs->rg.npts = m;
+    std::vector<RangedFilter> d;
+    for (uint32_t j = 0; j < live.size(); j++) {
+        const auto* S = live[j];
         RangedFilter r;
         memset(&r, 0, sizeof r);
-        r.f.words32 = (const uint32_t*)S.words.p;
-        r.f.md = Mod32::make(S.num_bits ? S.num_bits : 1);
-        r.f.num_bits = S.num_bits;
-        r.f.k = S.k;
-        r.f.out_bit = s;
-        r.f.group = s;
-        r.lo = rb + at[j].first;
-        r.hi = rb + at[j].second;
-        r.lo_len = (uint32_t)S.lo.size();
-        r.hi_len = (uint32_t)S.hi.size();
+        r.f.words32 = (const uint32_t*)S->words.p;
+        r.f.md = Mod32::make(S->num_bits ? S->num_bits : 1);
+        r.f.num_bits = S->num_bits;
+        r.f.k = S->k;
+        r.f.out_bit = slot_of[j];
+        r.f.group = slot_of[j];
         d.push_back(r);
-        j++;
     }
     HIP_TRY(fs->desc.ensure(sizeof(RangedFilter) * 64));
     if (!d.empty())
         HIP_TRY(hipMemcpyAsync(fs->desc.p, d.data(), sizeof(RangedFilter) * d.size(), hipMemcpyHostToDevice, fs->ust));
-    HIP_TRY(hipStreamSynchronize(fs->ust));  // blob and d are host temporaries
+    HIP_TRY(hipStreamSynchronize(fs->ust));  // blob, pbuf and d are host temporaries
     fs->ndesc = (uint32_t)d.size();
     fs->shared_nb = d.empty() ? 0 : d[0].f.num_bits;
     fs->shared_k = d.empty() ? 0 : d[0].f.k;
@@ -980,6 +1025,7 @@ void lsmb_fset_close(lsmb_fset* fs) {
         if (fs->ust) hipStreamSynchronize(fs->ust), hipStreamDestroy(fs->ust);
         for (auto& S : fs->slot) S.words.release();
         fs->ranges.release();
+        fs->points.release();
         fs->desc.release();
     }
     delete fs;
@@ -1029,7 +1075,8 @@ int lsmb_fset_probe_dev(lsmb_fset* fs, const void* d_data, const void* d_offsets
         return LSMB_OK;
     }
     KeyBatch kb{(const uint8_t*)d_data, (const uint64_t*)d_offsets, key_len, n};
-    HIP_TRY(launch_fset_probe(kb, (const RangedFilter*)fs->desc.p, fs->ndesc, fs->shared_nb, fs->shared_k, (uint64_t*)d_out, fs->c->num_cus, st));
+    HIP_TRY(launch_fset_probe(kb, (const RangedFilter*)fs->desc.p, fs->ndesc, fs->rg, fs->shared_nb, fs->shared_k,
+                              (uint64_t*)d_out, fs->c->num_cus, st));
     return fset_note_probe(fs, st);
 }
 
@@ -1049,7 +1096,8 @@ int lsmb_fset_probe(lsmb_fset* fs, const uint8_t* data, const uint64_t* offsets,
         memset(out_mask, 0, n * 8);
         return LSMB_OK;
     }
-    HIP_TRY(launch_fset_probe(kb, (const RangedFilter*)fs->desc.p, fs->ndesc, fs->shared_nb, fs->shared_k, (uint64_t*)c->out.p, c->num_cus, c->st));
+    HIP_TRY(launch_fset_probe(kb, (const RangedFilter*)fs->desc.p, fs->ndesc, fs->rg, fs->shared_nb, fs->shared_k,
+                              (uint64_t*)c->out.p, c->num_cus, c->st));
     if (int rc = fset_note_probe(fs, c->st)) return rc;
     HIP_TRY(hipMemcpyAsync(out_mask, c->out.p, n * 8, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(hipStreamSynchronize(c->st));

@@ -112,12 +112,30 @@ struct RangedFilter {
     uint32_t lo_len, hi_len;
 };
 
+// The key ranges of a filter set as sorted boundary points (built on the host
+// per set): the distinct min/max keys of the live tables in Rust [u8] order.
+// For a key, region 2r = strictly between points r-1 and r, region 2r+1 =
+// equal to point r; regmask[region] = the descriptors (bit d = descriptor d)
+// whose [min_key, max_key] holds every key of that region.  So the range
+// pre-check of all F tables is one rank search over <= 2F points.
+constexpr uint32_t kFsetMaxPoints = 128;
+struct FsetPoint {
+    uint64_t w0, w1;   // zero-padded 16-byte prefix as two big-endian words
+    const uint8_t* p;  // the full key (device memory)
+    uint32_t len, pad;
+};
+struct FsetRanges {
+    const FsetPoint* pts;     // npts, sorted
+    const uint64_t* regmask;  // 2 * npts + 1
+    uint32_t npts;
+};
+
 // out[i] bit s = (lo_s <= key i <= hi_s) && may_contain(filter s, key i), for
 // the nfilt (<= 64) descriptors at d_filters (device memory).  shared_nb /
 // shared_k: the (num_bits, k) every descriptor has, or 0 when they differ
 // (selects the bit-sliced LDS table).
-hipError_t launch_fset_probe(const KeyBatch& kb, const RangedFilter* d_filters, uint32_t nfilt, uint32_t shared_nb,
-                             uint32_t shared_k, uint64_t* d_out, int num_cus, hipStream_t st);
+hipError_t launch_fset_probe(const KeyBatch& kb, const RangedFilter* d_filters, uint32_t nfilt, const FsetRanges& rg,
+                             uint32_t shared_nb, uint32_t shared_k, uint64_t* d_out, int num_cus, hipStream_t st);
 
 hipError_t launch_probe(const KeyBatch& kb, const ProbeFilter* h_filters, uint32_t nfilt,
                         ProbeFilter* d_filters_scratch, uint8_t* d_out, int num_cus,

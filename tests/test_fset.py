@@ -186,16 +186,19 @@ def test_fset_add_rejects_corrupt_blocks_like_deserialize(oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("ntab,fpr", [(5, 0.05), (20, 0.01), (33, 0.001)])
-def test_fset_same_sized_sliced_table_widths(oracle, ntab, fpr):
+@pytest.mark.parametrize("ntab,n,fpr", [(5, 800, 0.05), (12, 800, 0.01), (20, 800, 0.01), (33, 800, 0.001),
+                                        (40, 500, 0.01), (64, 500, 0.01)])
+def test_fset_same_sized_sliced_table_widths(oracle, ntab, n, fpr):
     # every filter of the set shares (num_bits, k): the bit-sliced LDS table
-    # path, at 8/32/64-bit entries and k != 7
+    # path at 8/16/32/64-bit entries (after removing slot 1: 4, 11, 19 / 32,
+    # 39 and 63 filters; each table within 64 KiB of LDS) and k != 7, with a
+    # non-identity slot -> output-bit mapping (slot 1 is gone)
     ctx = lsmbloom.Context(0)
     fs = FilterSet(ctx)
-    nb, k = lsmbloom.params(800, fpr)
+    nb, k = lsmbloom.params(n, fpr)
     tables = {}
     for t in range(ntab):
-        keys = keygen.key16(0x5EED0500 + t, 0, 800)
+        keys = keygen.key16(0x5EED0500 + t, 0, n)
         rows = sorted(bytes(r) for r in keys)
         w = oracle.build_fixed(keys, 16, nb, k)
         lo, hi = rows[t % 3 * 100], rows[-1 - t % 5 * 100]
@@ -231,6 +234,52 @@ def test_fset_bounds_sharing_16_byte_prefixes(oracle):
             oracle.insert(w, nb, k, key)  # every query a member: the range decides
         s = fs.add_filter(BloomFilter(w, k, nb), lo, hi)
         tables[s] = (w, nb, k, lo, hi)
+    got = fs.probe_keys(q)
+    assert [int(x) for x in got] == expected_masks(oracle, tables, q)
+    fs.close()
+    ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mixed", [False, True])
+def test_fset_random_ranges_region_lookup(oracle, mixed):
+    """The range pre-check as one rank search over the sorted distinct bounds:
+    random ranges with shared bounds, empty ranges (min > max), single-key
+    ranges, and queries equal to / between / outside the bounds, with var-len
+    keys up to 40 bytes (16-byte prefix ties resolved by the full compare).
+    Same-sized filters take the sliced kernel, mixed sizes the per-filter one."""
+    rng = np.random.default_rng(11 + mixed)
+    ctx = lsmbloom.Context(0)
+    fs = FilterSet(ctx)
+    alphabet = [b"", b"a", b"ab", b"0123456789abcdef", b"0123456789abcdef\x00", b"0123456789abcdefz",
+                b"0123456789abcdefzz" * 2, b"b", b"zz", b"\xff" * 17]
+
+    def rnd_key():
+        base = alphabet[rng.integers(len(alphabet))]
+        return base + bytes(rng.integers(0, 256, size=rng.integers(0, 4), dtype=np.uint8))
+
+    q = [rnd_key() for _ in range(3000)]
+    tables = {}
+    for t in range(30):
+        a, b = rnd_key(), rnd_key()
+        if t % 7 == 0:
+            b = a  # single-key range
+        if t % 5 == 0 and a < b:
+            a, b = b, a  # empty range: min > max holds no key
+        if t % 4 == 1 and tables:
+            a = list(tables.values())[0][3]  # a shared bound
+        n = 100 if not mixed else [100, 5000, 20000][t % 3]
+        nb, k = lsmbloom.params(n, 0.01)
+        w = np.zeros(lsmbloom.num_words(nb), np.uint64)
+        for key in q[t::7]:
+            oracle.insert(w, nb, k, key)
+        s = fs.add_filter(BloomFilter(w, k, nb), a, b)
+        tables[s] = (w, nb, k, a, b)
+    got = fs.probe_keys(q)
+    assert [int(x) for x in got] == expected_masks(oracle, tables, q)
+    for s in (3, 17):
+        fs.remove(s)
+        del tables[s]
     got = fs.probe_keys(q)
     assert [int(x) for x in got] == expected_masks(oracle, tables, q)
     fs.close()

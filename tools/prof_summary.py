@@ -36,7 +36,10 @@ def traffic_json(d, out):
             kern[kn] = {"read_bytes": int(2 * m.get("FETCH_SIZE", 0) * 1024),
                         "write_bytes": int(m.get("WRITE_SIZE", 0) * 1024)}
     tot = sum(v["read_bytes"] + v["write_bytes"] for v in kern.values())
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench  # the sha of the build kernels' sources this profile measured
     json.dump({"profile": os.path.basename(d.rstrip("/")), "build_bytes": tot, "kernels": kern,
+               "kernel_src_sha": bench.build_sources_sha(),
                "note": "FETCH_SIZE x2 (gfx950), KiB -> B; mean per dispatch over separate --pmc passes"},
               open(out, "w"), indent=1)
 

@@ -8,7 +8,7 @@ REPO=${GRAFT_REPO_ROOT:-/root/repo}
 OUT=$REPO/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-BENCH="$REPO/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e --no-varlen $*"
+BENCH="$REPO/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e --no-varlen --no-exact10 $*"
 run() {  # name, rocprofv3 args...
   local name=$1; shift
   timeout -k 10 300 rocprofv3 "$@" --output-format csv -d "$OUT/$name" -o run -- python3 $BENCH > "$OUT/$name.log" 2>&1
@@ -20,6 +20,8 @@ run sq1 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_
 run sq2 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_BUSY_CYCLES
 # C4 var-len build kernels (k_bin<ks::VarLen...>, k_apply), kernel trace only
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats_c4" -o run -- \
-    python3 $REPO/bench.py --steps 6 --warmup 2 --no-cpu-baseline --no-e2e --no-probe --keys-per-gpu 1000000 \
+    python3 $REPO/bench.py --steps 6 --warmup 2 --no-cpu-baseline --no-e2e --no-probe --no-exact10 --keys-per-gpu 1000000 \
     > "$OUT/stats_c4.log" 2>&1
+python3 $REPO/tools/prof_summary.py "$OUT" > "$OUT/summary.md"
+python3 $REPO/tools/prof_summary.py "$OUT" --json "$OUT/traffic.json"
 echo "profile $TAG done"
