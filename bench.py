@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory end-to-end measurement")
     ap.add_argument("--no-varlen", action="store_true", help="skip the C4 variable-length build leg")
     ap.add_argument("--no-exact10", action="store_true", help="skip the C2 exact 10 bits/key leg")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="N > 1: build the whole filter, then OR-allreduce it (no per-sweep overlap)")
     ap.add_argument("--varlen-keys", type=int, default=100_000_000)
     ap.add_argument("--filter-keys", type=int, default=0, help="size the filter for this many keys (default: the global run)")
     return ap.parse_args()
@@ -240,6 +242,30 @@ def main():
         if world > 1:
             ldist.or_allreduce_(words, ctx=ctx)
 
+    # N > 1 step: the partitioned build runs in sweeps (C5: 4 x 64 MiB word
+    # ranges); sweep s's range is final when its pass B ends, so its OR-allreduce
+    # runs on a side stream while sweep s+1 builds (lsmb_build_fixed_dev_sweep).
+    nsw = lsmbloom.build_sweeps(nb, npg, k)
+    ranges = [lsmbloom.sweep_words(nb, npg, s, k) for s in range(nsw)]
+    overlap = world > 1 and nsw > 1 and not args.no_overlap
+    side = torch.cuda.Stream(dev) if overlap else None
+    sweep_ev = [torch.cuda.Event() for _ in range(nsw)]
+
+    def step():
+        if not overlap:
+            build()
+            allreduce()
+            return
+        words.zero_()
+        main = torch.cuda.current_stream(dev)
+        for s, (a, b) in enumerate(ranges):
+            ctx.build_fixed_dev_sweep(keys, 16, npg, nb, k, words, s)
+            sweep_ev[s].record(main)
+            side.wait_event(sweep_ev[s])
+            with torch.cuda.stream(side):
+                ldist.or_allreduce_(words[a:b], ctx=ctx)
+        main.wait_stream(side)
+
     def barrier():
         if world > 1:
             dist.barrier()
@@ -254,24 +280,33 @@ def main():
 
     ctx.set_timing(False)  # no timing markers between the kernels of a timed step
     for _ in range(args.warmup):
-        build()
-        allreduce()
+        step()
     barrier()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
-    for e0, e1, e2 in ev:
-        e0.record()
-        build()
-        e1.record()
-        allreduce()
-        e2.record()
+    for _ in range(args.steps):
+        step()
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0)
     ms = dt / args.steps * 1e3
     value = total * args.steps / dt / 1e6
-    build_ms = max_over_ranks(sum(a.elapsed_time(b) for a, b, _ in ev) / args.steps)
-    coll_ms = max_over_ranks(sum(b.elapsed_time(c) for _, b, c in ev) / args.steps)
+    build_ms = coll_ms = serial_ms = 0.0
+    if world > 1:
+        # Split (outside the timed region): the same steps run serially —
+        # build, then the full-filter OR-allreduce — timed by events.
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+               torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        barrier()
+        t1 = time.perf_counter()
+        for e0, e1, e2 in ev:
+            e0.record()
+            build()
+            e1.record()
+            allreduce()
+            e2.record()
+        barrier()
+        serial_ms = max_over_ranks(time.perf_counter() - t1) / args.steps * 1e3
+        build_ms = max_over_ranks(sum(a.elapsed_time(b) for a, b, _ in ev) / args.steps)
+        coll_ms = max_over_ranks(sum(b.elapsed_time(c) for _, b, c in ev) / args.steps)
 
     # per-kernel times (HIP events on the build stream), averaged over `steps` builds
     ctx.set_timing(True)
@@ -310,16 +345,20 @@ def main():
         moved = 2 * (world - 1) / world * 8 * nw
         out["config"]["backend"] = args.backend
         out["step_split"] = {"build_ms": round(build_ms, 4), "or_allreduce_ms": round(coll_ms, 4),
-                             "what": "per step, slowest rank: zero + device build / bitwise-OR allreduce "
-                                     "(all_to_all reduce-scatter + native OR kernel + all_gather)",
+                             "what": "serial steps (untimed pass), slowest rank: zero + device build / "
+                                     "bitwise-OR allreduce (all_to_all reduce-scatter + native OR kernel "
+                                     "+ all_gather) of the whole filter",
+                             "serial_ms_per_step": round(serial_ms, 4),
+                             "timed_step": ("%d build sweeps, each sweep's word range OR-allreduced on a side "
+                                            "stream while the next sweep builds" % nsw) if overlap
+                                           else "build then OR-allreduce",
                              "or_allreduce_bytes_per_gpu": int(moved),
                              "or_allreduce_GBs_per_gpu": round(moved / (coll_ms * 1e-3) / 1e9, 1) if coll_ms else None}
         # Self-check (outside the timed region): one more sharded step; rank 0
         # then rebuilds the whole global key set alone, shard by shard, and
         # compares every word.  Its build time is the 1-GPU time of this same
         # workload (C5 on one GPU), for the strong-scaling curve.
-        build()
-        allreduce()
+        step()
         torch.cuda.synchronize(dev)
         if rank == 0:
             try:

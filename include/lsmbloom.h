@@ -201,6 +201,20 @@ int lsmb_build_fixed_dev(lsmb_ctx* ctx, const void* d_keys, uint32_t key_len, ui
 int lsmb_build_var_dev(lsmb_ctx* ctx, const void* d_data, const void* d_offsets, uint64_t n,
                        uint32_t num_bits, uint32_t num_hashes, void* d_words, void* stream);
 
+/* A partitioned build (filters above a few MiB) runs in sweeps: each re-reads
+ * the keys and keeps the positions of its own range of the filter (C5's
+ * 2^32-1-bit filter: 4 sweeps of 64 MiB).  lsmb_build_sweeps gives their
+ * number (1 for every other strategy), lsmb_sweep_words the word range
+ * [word_lo, word_hi) whose bits sweep s completes, and
+ * lsmb_build_fixed_dev_sweep builds just that sweep (OR-accumulate; running
+ * every sweep == lsmb_build_fixed_dev).  A sharded build can then merge sweep
+ * s's word range across GPUs while sweep s+1 builds. */
+int lsmb_build_sweeps(uint32_t num_bits, uint32_t num_hashes, uint64_t n);
+int lsmb_sweep_words(uint32_t num_bits, uint32_t num_hashes, uint64_t n, int sweep, uint64_t* word_lo,
+                     uint64_t* word_hi);
+int lsmb_build_fixed_dev_sweep(lsmb_ctx* ctx, const void* d_keys, uint32_t key_len, uint64_t n,
+                               uint32_t num_bits, uint32_t num_hashes, void* d_words, int sweep, void* stream);
+
 /* d_filt_words: host array of nfilt DEVICE pointers. */
 int lsmb_probe_dev(lsmb_ctx* ctx, const void* const* d_filt_words, const uint32_t* filt_bits,
                    const uint32_t* filt_hashes, uint32_t nfilt, const void* d_data,

@@ -586,12 +586,13 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
 __global__ __launch_bounds__(kApplyBlock) void k_apply(const uint64_t* __restrict__ regions,
                                                        const uint32_t* __restrict__ counts,
                                                        uint32_t grid, uint32_t cap, uint32_t nbins,
-                                                       uint32_t* __restrict__ gw, uint64_t nw32) {
+                                                       uint32_t* __restrict__ gw, uint64_t nw32,
+                                                       uint32_t bfirst, uint32_t bend) {
     __shared__ uint32_t filt[kSliceWords32];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr uint32_t NWAVE = kApplyBlock / 64;
     constexpr uint32_t PER = kSliceWords32 / 2 / kApplyBlock;  // u64 words per thread
-    for (uint32_t b = blockIdx.x; b < nbins; b += gridDim.x) {
+    for (uint32_t b = bfirst + blockIdx.x; b < bend; b += gridDim.x) {
         const uint64_t w0 = (uint64_t)b * kSliceWords32;
         const uint32_t nw2 = (uint32_t)min((uint64_t)kSliceWords32, nw32 - w0) / 2;  // u64 words
         uint2* g2 = reinterpret_cast<uint2*>(gw + w0);
@@ -713,8 +714,11 @@ void set_max_lds(const void* fn) {
 template <class Src>
 hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k, uint32_t* gw,
                       BuildStrategy s, const PartitionWorkspace& ws, int num_cus, hipStream_t st,
-                      BuildTimers* tm, bool t0_done = false) {
+                      BuildTimers* tm, int sweep, bool t0_done = false) {
     const Mod32 md = Mod32::make(num_bits);
+    // sweep >= 0 (partition builds): only that sweep's slices — pass A keeps
+    // their positions, pass B applies them; every other strategy has one sweep
+    if (sweep > 0 && s != BuildStrategy::Partition) return hipSuccess;
     const uint32_t nw32 = (uint32_t)(2 * (((uint64_t)num_bits + 63) / 64));
     if (tm && !t0_done) hipEventRecord(tm->t0, st);
     if (s == BuildStrategy::Lds) {
@@ -766,12 +770,13 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
         else
             k_hash<Src><<<dim3((uint32_t)g), dim3(256), 0, st>>>(src, n, ws.hashes);
         // pass A's timer (t1) covers k_hash + k_bin
-        return build_with(Hashed{ws.hashes}, n, num_bits, k, gw, s, ws, num_cus, st, tm, /*t0_done=*/true);
+        return build_with(Hashed{ws.hashes}, n, num_bits, k, gw, s, ws, num_cus, st, tm, sweep, /*t0_done=*/true);
     } else {
         const PartitionPlan pl = plan_partition(num_bits, k, n, num_cus);
         if (pl.region_bytes > ws.region_bytes || pl.counts_bytes > ws.counts_bytes) return hipErrorInvalidValue;
         const bool w32 = fits_walk32(num_bits);
         for (uint32_t sw = 0; sw < pl.sweeps; sw++) {
+            if (sweep >= 0 && sw != (uint32_t)sweep) continue;
             PassA a;
             a.b0 = sw * pl.bins_per_sweep;
             a.nb = min(pl.bins_per_sweep, pl.nbins - a.b0);
@@ -813,8 +818,11 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
             if (e != hipSuccess) return e;
         }
         if (tm) hipEventRecord(tm->t1, st);
-        k_apply<<<dim3(pl.nbins), dim3(kApplyBlock), 0, st>>>(ws.regions, ws.counts, pl.grid, pl.cap_segs,
-                                                              pl.nbins, gw, nw32);
+        const uint32_t bfirst = sweep >= 0 ? (uint32_t)sweep * pl.bins_per_sweep : 0u;
+        const uint32_t bend = sweep >= 0 ? min(pl.nbins, bfirst + pl.bins_per_sweep) : pl.nbins;
+        if (bend > bfirst)
+            k_apply<<<dim3(bend - bfirst), dim3(kApplyBlock), 0, st>>>(ws.regions, ws.counts, pl.grid, pl.cap_segs,
+                                                                       pl.nbins, gw, nw32, bfirst, bend);
     }
     if (tm) {
         hipEventRecord(tm->t2, st);
@@ -928,13 +936,13 @@ uint64_t partition_chunk_keys(uint32_t num_bits, uint32_t k, uint64_t max_bytes,
 
 hipError_t launch_build(const KeyBatch& kb, uint32_t num_bits, uint32_t k, uint32_t* gw,
                         BuildStrategy s, const PartitionWorkspace& ws, int num_cus, hipStream_t st,
-                        BuildTimers* tm) {
+                        BuildTimers* tm, int sweep) {
     if (s == BuildStrategy::None) return hipSuccess;
-    if (kb.offsets) return build_with(VarLen{kb.data, kb.offsets}, kb.n, num_bits, k, gw, s, ws, num_cus, st, tm);
+    if (kb.offsets) return build_with(VarLen{kb.data, kb.offsets}, kb.n, num_bits, k, gw, s, ws, num_cus, st, tm, sweep);
     if (kb.key_len == 16 && (reinterpret_cast<uintptr_t>(kb.data) & 15) == 0)
         return build_with(Fixed16{reinterpret_cast<const uint4*>(kb.data)}, kb.n, num_bits, k, gw, s, ws,
-                          num_cus, st, tm);
-    return build_with(FixedN{kb.data, kb.key_len}, kb.n, num_bits, k, gw, s, ws, num_cus, st, tm);
+                          num_cus, st, tm, sweep);
+    return build_with(FixedN{kb.data, kb.key_len}, kb.n, num_bits, k, gw, s, ws, num_cus, st, tm, sweep);
 }
 
 hipError_t launch_or_reduce(uint32_t* dst, const uint32_t* src, uint64_t nw32, uint32_t nsrc,

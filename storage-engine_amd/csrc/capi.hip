@@ -109,12 +109,12 @@ int check_device_error(lsmb_ctx* c) {
 
 namespace {
 int build_dev_ws(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k, uint32_t* dw, hipStream_t st,
-                 BuildStrategy s);
+                 BuildStrategy s, int sweep);
 }  // namespace
 
 // Device build of one batch, chunked so the partition workspace stays bounded.
 int build_dev(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k, uint32_t* dw,
-              hipStream_t st) {
+              hipStream_t st, int sweep) {
     BuildStrategy s = pick_build_strategy(num_bits, k, kb_all.n);
     // LSMB_FORCE_STRATEGY=atomic: measurement override;
     // the filter is the same either way.
@@ -123,12 +123,12 @@ int build_dev(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k
     c->tm.valid = false;
     if (s == BuildStrategy::None) return LSMB_OK;
     if (s != BuildStrategy::Tiled && s != BuildStrategy::Partition)
-        return build_dev_ws(c, kb_all, num_bits, k, dw, st, s);
+        return build_dev_ws(c, kb_all, num_bits, k, dw, st, s, sweep);
     // Tiled and partition builds use the context's shared workspace: a build
     // issued on a different stream than the last one waits for it (two
     // streams' builds would otherwise overwrite each other's regions).
     if (c->ws_stream) HIP_TRY(hipStreamWaitEvent(st, c->ws_done, 0));
-    const int rc = build_dev_ws(c, kb_all, num_bits, k, dw, st, s);
+    const int rc = build_dev_ws(c, kb_all, num_bits, k, dw, st, s, sweep);
     HIP_TRY(hipEventRecord(c->ws_done, st));
     c->ws_stream = st;
     return rc;
@@ -136,7 +136,7 @@ int build_dev(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k
 
 namespace {
 int build_dev_ws(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k, uint32_t* dw, hipStream_t st,
-                 BuildStrategy s) {
+                 BuildStrategy s, int sweep) {
     if (s == BuildStrategy::Tiled) {
         const TiledPlan tp = plan_tiled(num_bits, kb_all.n, c->num_cus);
         HIP_TRY(c->ws_regions.ensure(tp.scratch_bytes));
@@ -148,11 +148,12 @@ int build_dev_ws(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_
             ws.hashes = (uint4*)c->ws_hashes.p;
             ws.hash_bytes = c->ws_hashes.bytes;
         }
-        HIP_TRY(launch_build(kb_all, num_bits, k, dw, s, ws, c->num_cus, st, c->timing ? &c->tm : nullptr));
+        HIP_TRY(launch_build(kb_all, num_bits, k, dw, s, ws, c->num_cus, st, c->timing ? &c->tm : nullptr, sweep));
         return LSMB_OK;
     }
     if (s != BuildStrategy::Partition) {
-        HIP_TRY(launch_build(kb_all, num_bits, k, dw, s, PartitionWorkspace{}, c->num_cus, st, c->timing ? &c->tm : nullptr));
+        HIP_TRY(launch_build(kb_all, num_bits, k, dw, s, PartitionWorkspace{}, c->num_cus, st,
+                             c->timing ? &c->tm : nullptr, sweep));
         return LSMB_OK;
     }
     c->ran_partition = true;
@@ -181,7 +182,7 @@ int build_dev_ws(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_
             kb.offsets += first;  // VarLen offsets are absolute into data
         else
             kb.data += first * kb.key_len;
-        HIP_TRY(launch_build(kb, num_bits, k, dw, s, ws, c->num_cus, st, c->timing ? &c->tm : nullptr));
+        HIP_TRY(launch_build(kb, num_bits, k, dw, s, ws, c->num_cus, st, c->timing ? &c->tm : nullptr, sweep));
     }
     return LSMB_OK;
 }
@@ -605,6 +606,40 @@ static int need_ctx(lsmb_ctx* c, uint64_t n) {
                     (unsigned long long)host_max_keys());
     (void)n;
     return LSMB_OK;
+}
+
+int lsmb_build_sweeps(uint32_t num_bits, uint32_t k, uint64_t n) {
+    if (pick_build_strategy(num_bits, k, n) != BuildStrategy::Partition) return 1;
+    return (int)plan_partition(num_bits, k, n, 256).sweeps;
+}
+
+int lsmb_sweep_words(uint32_t num_bits, uint32_t k, uint64_t n, int sweep, uint64_t* word_lo, uint64_t* word_hi) {
+    if (!word_lo || !word_hi) return fail(LSMB_EINVAL, "null output pointer");
+    const int ns = lsmb_build_sweeps(num_bits, k, n);
+    if (sweep < 0 || sweep >= ns) return fail(LSMB_EINVAL, "sweep %d out of range [0, %d)", sweep, ns);
+    const uint64_t nw = nwords64(num_bits);
+    if (ns == 1) {
+        *word_lo = 0;
+        *word_hi = nw;
+        return LSMB_OK;
+    }
+    const PartitionPlan pl = plan_partition(num_bits, k, n, 256);
+    const uint64_t w_per_slice = (1ull << kSliceLog2) / 64;
+    *word_lo = std::min<uint64_t>(nw, (uint64_t)sweep * pl.bins_per_sweep * w_per_slice);
+    *word_hi = std::min<uint64_t>(nw, ((uint64_t)sweep + 1) * pl.bins_per_sweep * w_per_slice);
+    return LSMB_OK;
+}
+
+int lsmb_build_fixed_dev_sweep(lsmb_ctx* c, const void* d_keys, uint32_t key_len, uint64_t n, uint32_t num_bits,
+                               uint32_t k, void* d_words, int sweep, void* stream) {
+    if (!c) return fail(LSMB_EINVAL, "null ctx");
+    if (int rc = check_filter(num_bits, k)) return rc;
+    if (n && (!d_keys || !d_words)) return fail(LSMB_EINVAL, "null device pointer");
+    const int ns = lsmb_build_sweeps(num_bits, k, n);
+    if (sweep < 0 || sweep >= ns) return fail(LSMB_EINVAL, "sweep %d out of range [0, %d)", sweep, ns);
+    DevGuard g(c->dev);
+    KeyBatch kb{(const uint8_t*)d_keys, nullptr, key_len, key_len ? n : (n ? 1 : 0)};
+    return build_dev(c, kb, num_bits, k, (uint32_t*)d_words, pick_stream(c, stream), sweep);
 }
 
 int lsmb_build_fixed(lsmb_ctx* c, const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t num_bits,

@@ -110,7 +110,8 @@ namespace lsmb {
 
 // Device build of one batch on `st` into d_words (OR-accumulate), chunked so
 // the partition workspace stays bounded.  Asynchronous.
-int build_dev(lsmb_ctx* c, const KeyBatch& kb, uint32_t num_bits, uint32_t k, uint32_t* d_words, hipStream_t st);
+int build_dev(lsmb_ctx* c, const KeyBatch& kb, uint32_t num_bits, uint32_t k, uint32_t* d_words, hipStream_t st,
+              int sweep = -1);
 
 // Keys in host memory -> OR-accumulated into the device words dw (already
 // zeroed or loaded by the caller) on c->st: chunked H2D through the two

@@ -88,10 +88,12 @@ struct BuildTimers {
 
 // Builds into d_words32 (OR-accumulate).  For the Partition strategy the
 // workspace must hold plan_partition(num_bits, k, kb.n, num_cus).  Records
-// t0/t1/t2 (start / pass A done / end) when timers != NULL.
+// t0/t1/t2 (start / pass A done / end) when timers != NULL.  sweep >= 0
+// builds only the bits of that partition sweep's slices (sweep 0 = the whole
+// build for the other strategies; see build_sweeps / sweep_words).
 hipError_t launch_build(const KeyBatch& kb, uint32_t num_bits, uint32_t k, uint32_t* d_words32,
                         BuildStrategy s, const PartitionWorkspace& ws, int num_cus,
-                        hipStream_t st, BuildTimers* timers);
+                        hipStream_t st, BuildTimers* timers, int sweep = -1);
 
 // Filter descriptor for the probe kernels (device-side array).
 struct ProbeFilter {

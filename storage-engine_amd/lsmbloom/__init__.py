@@ -80,6 +80,10 @@ SIGNATURES = {
     "lsmb_fset_probe_dev": (ctypes.c_int, [vp, vp, vp, ctypes.c_uint32, ctypes.c_uint64, vp, vp]),
     "lsmb_build_strategy": (ctypes.c_char_p, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]),
     "lsmb_host_max_keys": (ctypes.c_uint64, []),
+    "lsmb_build_sweeps": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]),
+    "lsmb_sweep_words": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, u64p, u64p]),
+    "lsmb_build_fixed_dev_sweep": (ctypes.c_int, [vp, vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
+                                                  ctypes.c_uint32, vp, ctypes.c_int, vp]),
     "lsmb_set_host_max_keys": (None, [ctypes.c_uint64]),
     "lsmb_multi_open": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     "lsmb_multi_close": (None, [vp]),
@@ -283,6 +287,11 @@ class Context:
         _check(lib().lsmb_build_fixed_dev(self.h, vp(keys.data_ptr()), key_len, n, num_bits, k,
                                           vp(words.data_ptr()), self._stream(stream)))
 
+    def build_fixed_dev_sweep(self, keys, key_len, n, num_bits, k, words, sweep, stream=None):
+        """One sweep of a partitioned build (lsmb_build_fixed_dev_sweep)."""
+        _check(lib().lsmb_build_fixed_dev_sweep(self.h, vp(keys.data_ptr()), key_len, n, num_bits, k,
+                                                vp(words.data_ptr()), int(sweep), self._stream(stream)))
+
     def build_var_dev(self, data, offsets, n, num_bits, k, words, stream=None):
         _check(lib().lsmb_build_var_dev(self.h, vp(data.data_ptr()), vp(offsets.data_ptr()), n, num_bits, k,
                                         vp(words.data_ptr()), self._stream(stream)))
@@ -467,6 +476,18 @@ class FilterSet:
 def build_strategy(num_bits, n, k=7):
     """Device build strategy for (num_bits, k, n): lds / tiled / partition / atomic."""
     return lib().lsmb_build_strategy(num_bits, k, n).decode()
+
+
+def build_sweeps(num_bits, n, k=7):
+    """Sweeps of the device build of n keys (1 unless partitioned in several)."""
+    return int(lib().lsmb_build_sweeps(num_bits, k, n))
+
+
+def sweep_words(num_bits, n, sweep, k=7):
+    """[word_lo, word_hi): the filter words whose bits sweep `sweep` completes."""
+    lo, hi = ctypes.c_uint64(), ctypes.c_uint64()
+    _check(lib().lsmb_sweep_words(num_bits, k, n, int(sweep), ctypes.byref(lo), ctypes.byref(hi)))
+    return lo.value, hi.value
 
 
 def host_max_keys():

@@ -159,3 +159,22 @@ def test_no_device_wide_synchronisation_in_library():
         assert "hipDeviceSynchronize" not in code, path
         assert not re.search(r"\bhipMemcpy\s*\(", code), path
         assert not re.search(r"\bhipMemset\s*\(", code), path
+
+
+def test_sweep_ranges_tile_the_filter():
+    """lsmb_build_sweeps / lsmb_sweep_words (host-only planning): the sweeps'
+    word ranges are contiguous, disjoint and cover the filter; C5's 2^32-1-bit
+    filter runs in 4 sweeps of 2^24 words, everything C2-sized in one."""
+    for filter_n, n, want in [(1_000_000_000, 125_000_000, 4), (1_000_000_000, 2_000_000, 4),
+                              (100_000_000, 100_000_000, 1), (1000, 1000, 1)]:
+        nb, k = lsmbloom.params(filter_n, 0.01)
+        ns = lsmbloom.build_sweeps(nb, n, k)
+        assert ns == want
+        at = 0
+        for s in range(ns):
+            lo, hi = lsmbloom.sweep_words(nb, n, s, k)
+            assert lo == at and hi > lo
+            at = hi
+        assert at == lsmbloom.num_words(nb)
+        with pytest.raises(ValueError):
+            lsmbloom.sweep_words(nb, n, ns, k)

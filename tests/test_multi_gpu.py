@@ -98,6 +98,35 @@ def test_multi_build_fixed_dev_or_accumulates(torch, oracle):
         m.close()
 
 
+@pytest.mark.parametrize("filter_n,n", [(1_000_000_000, 2_000_000),   # C5's filter: 4 sweeps
+                                         (1_000_000, 1_000_000)])        # one sweep (tiled)
+def test_sweep_builds_cover_the_filter(torch, ctx, oracle, filter_n, n):
+    """lsmb_build_fixed_dev_sweep: sweep s sets only the bits of its word range
+    (lsmb_sweep_words) and every sweep together == the whole build — the
+    property the N > 1 bench leans on to OR-allreduce range s while s+1 builds."""
+    nb, k = lsmbloom.params(filter_n, 0.01)
+    nw = lsmbloom.num_words(nb)
+    dev = torch.device("cuda:0")
+    host = keygen.key16(0x5EED0001, 0, n)
+    keys = torch.from_numpy(np.ascontiguousarray(host)).to(dev)
+    ref = oracle.build_fixed_mt(host, 16, nb, k, 8)
+    nsw = lsmbloom.build_sweeps(nb, n, k)
+    assert nsw == (4 if filter_n == 1_000_000_000 else 1)
+    acc = torch.zeros(nw, dtype=torch.int64, device=dev)
+    one = torch.zeros(nw, dtype=torch.int64, device=dev)
+    for s in range(nsw):
+        lo, hi = lsmbloom.sweep_words(nb, n, s, k)
+        one.zero_()
+        ctx.build_fixed_dev_sweep(keys, 16, n, nb, k, one, s)
+        ctx.build_fixed_dev_sweep(keys, 16, n, nb, k, acc, s)
+        got = _u64(one)
+        assert np.array_equal(got[lo:hi], ref[lo:hi]), "sweep %d's range differs" % s
+        assert not got[:lo].any() and not got[hi:].any(), "sweep %d wrote outside its range" % s
+    assert np.array_equal(_u64(acc), ref)
+    with pytest.raises(ValueError):
+        ctx.build_fixed_dev_sweep(keys, 16, n, nb, k, acc, nsw)
+
+
 @pytest.mark.parametrize("G", [1, 2, 3])
 def test_multi_build_block_fixed_and_varlen(oracle, G):
     m = lsmbloom.Multi([0] * G)
@@ -179,13 +208,17 @@ def test_dist_or_allreduce_device_path(oracle, world, n, filter_n):
         assert np.array_equal(mine[: end - start], ref[start:end])
 
 
-def test_bench_launches_its_own_ranks():
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("filter_keys", [None, 1_000_000_000])
+def test_bench_launches_its_own_ranks(filter_keys):
     """`python bench.py --gpus 2` (no torchrun) starts two ranks itself; here
     over gloo, both on cuda:0.  The line must say n_gpus 2, carry the split
     build / OR-allreduce timing, and the rank-0 word-for-word self-check."""
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
            "--global-keys", "8000000", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-e2e",
            "--no-varlen", "--no-exact10", "--probe-keys", "200000"]
+    if filter_keys:  # C5's 2^32-1-bit filter: 4 sweeps, per-range allreduce overlapped
+        cmd += ["--filter-keys", str(filter_keys), "--no-probe"]
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
@@ -197,7 +230,9 @@ def test_bench_launches_its_own_ranks():
     assert out["scaling"] == "strong" and out["config"]["keys_per_gpu"] == 4_000_000
     assert out["multi_gpu_merged_equals_single_gpu_build"] is True
     assert out["step_split"]["or_allreduce_ms"] > 0 and out["step_split"]["build_ms"] > 0
-    assert out["probe"]["member_rows_all_hit"] is True
+    if filter_keys:
+        assert out["step_split"]["timed_step"].startswith("4 build sweeps")
+    assert filter_keys or out["probe"]["member_rows_all_hit"] is True
 
 
 def test_bench_refuses_world_mismatch():
