@@ -242,7 +242,7 @@ def main():
         if world > 1:
             ldist.or_allreduce_(words, ctx=ctx)
 
-    # N > 1 step: the partitioned build runs in sweeps (C5: 4 x 64 MiB word
+    # N > 1 step: the partitioned build runs in sweeps (C5: 2 x 256 MiB word
     # ranges); sweep s's range is final when its pass B ends, so its OR-allreduce
     # runs on a side stream while sweep s+1 builds (lsmb_build_fixed_dev_sweep).
     nsw = lsmbloom.build_sweeps(nb, npg, k)

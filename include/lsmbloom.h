@@ -203,7 +203,7 @@ int lsmb_build_var_dev(lsmb_ctx* ctx, const void* d_data, const void* d_offsets,
 
 /* A partitioned build (filters above a few MiB) runs in sweeps: each re-reads
  * the keys and keeps the positions of its own range of the filter (C5's
- * 2^32-1-bit filter: 4 sweeps of 64 MiB).  lsmb_build_sweeps gives their
+ * 2^32-1-bit filter: 2 sweeps of 256 MiB).  lsmb_build_sweeps gives their
  * number (1 for every other strategy), lsmb_sweep_words the word range
  * [word_lo, word_hi) whose bits sweep s completes, and
  * lsmb_build_fixed_dev_sweep builds just that sweep (OR-accumulate; running

@@ -160,18 +160,22 @@ __device__ __forceinline__ void lds_barrier() {
     __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+template <int SL = kSliceLog2>
 __device__ __forceinline__ void or_pos_global(uint32_t* gw, uint32_t b, uint32_t off) {
-    const uint32_t p = (b << kSliceLog2) | off;
+    const uint32_t p = (b << SL) | off;
     atomicOr(gw + (p >> 5), 1u << (p & 31));
 }
 
-// Three 20-bit offsets in one u64: x | y << 20 | z << 40, built from 32-bit
-// shift-or instructions (no 64-bit shifts).
+// Three SL-bit offsets (SL = 20 or 21) in one u64: x | y << SL | z << 2 SL,
+// built from 32-bit shift-or instructions (no 64-bit shifts).
+template <int SL = kSliceLog2>
 __device__ __forceinline__ uint2 pack3w(uint32_t x, uint32_t y, uint32_t z) {
-    return make_uint2(x | (y << 20), (y >> 12) | (z << 8));
+    static_assert(SL == 20 || SL == 21, "3 offsets per u64");
+    return make_uint2(x | (y << SL), (y >> (32 - SL)) | (z << (2 * SL - 32)));
 }
+template <int SL = kSliceLog2>
 __device__ __forceinline__ uint64_t pack3(uint32_t x, uint32_t y, uint32_t z) {
-    const uint2 w = pack3w(x, y, z);
+    const uint2 w = pack3w<SL>(x, y, z);
     return ((uint64_t)w.y << 32) | w.x;
 }
 
@@ -207,9 +211,12 @@ constexpr uint32_t kAhead = 4;  // pass A key prefetch distance, in phases
 // PER: keys per lane per phase.  Sweeps (!FULL) keep ~1/sweeps of the
 // positions, so their phases take two keys per lane: half the barriers and
 // flush rounds per key (PartitionPlan::keys_per_lane; the ring is sized for it).
-template <class Src, class W, int KMAX, bool EXACT, bool FULL, int PER = 1>
+// SL: bin width log2 (20; 21 for sweeps of filters above 2^30 bits, whose
+// pass B applies each bin as two 2^20-bit halves).
+template <class Src, class W, int KMAX, bool EXACT, bool FULL, int PER = 1, int SL = kSliceLog2>
 __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md, uint32_t k_, PassA a) {
     static_assert(PER == 1 || EXACT, "two keys per lane: exact k only");
+    constexpr uint32_t kMask = (1u << SL) - 1;
     constexpr int NP = PER * KMAX;  // positions per lane per phase
     extern __shared__ uint32_t sm[];
     const uint32_t k = EXACT ? (uint32_t)KMAX : k_;
@@ -226,7 +233,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
         region_ptr(a, 0, w), 0, (int)(a.nbins * a.cap * 64u), 0x00020000);
     constexpr uint32_t kDrop = 0x80000000u;  // >= num_records (plan keeps it < 2^31)
     constexpr uint32_t kInc = 4u | (1u << 16);
-    const uint32_t sink = nb << kSliceLog2;  // local position of the sink slice
+    const uint32_t sink = nb << SL;  // local position of the sink slice
     const uint32_t lim = R << 16;            // fill < lim <=> claims < R
 
     // Workgroup w owns keys [w*per, (w+1)*per): a contiguous, coalesced run.
@@ -246,7 +253,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
 #pragma unroll
         for (int q = 0; q < KMAX; q++) {
             if (EXACT || (uint32_t)q < k) {
-                const uint32_t lp = walk.pos() - (FULL ? 0u : (a.b0 << kSliceLog2));
+                const uint32_t lp = walk.pos() - (FULL ? 0u : (a.b0 << SL));
                 out[q] = (FULL || lp < sink) ? lp : sink;
                 if (q + 1 < KMAX) walk.next(md);
             }
@@ -315,13 +322,13 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
         for (int q = 0; q < NP; q++) {
             if (EXACT || (uint32_t)q < k) {
                 if (FULL) {
-                    got[q] = (LSMB_ABL & 2) ? pos[q] : atomicAdd(fill + (pos[q] >> kSliceLog2), kinc[q / KMAX]);
+                    got[q] = (LSMB_ABL & 2) ? pos[q] : atomicAdd(fill + (pos[q] >> SL), kinc[q / KMAX]);
                 } else {
                     // A sweep keeps ~nb/nbins of the positions: the others are
                     // masked off rather than sent to the sink, whose single
                     // fill word and slot would serialise them (same-address
                     // LDS atomics and writes).
-                    got[q] = pos[q] < sink ? atomicAdd(fill + (pos[q] >> kSliceLog2), kInc) : 0u;
+                    got[q] = pos[q] < sink ? atomicAdd(fill + (pos[q] >> SL), kInc) : 0u;
                 }
             }
         }
@@ -370,14 +377,14 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
         auto slot = [&](int q) {
             uint32_t x = got[q] & 0xFFFFu;
             x = min(x, x - R4);
-            return __umul24(pos[q] >> kSliceLog2, R4) + x;
+            return __umul24(pos[q] >> SL, R4) + x;
         };
         if (__builtin_expect(__ballot(gmax >= lim) == 0, 1)) {
 #pragma unroll
             for (int q = 0; q < NP; q++) {
                 if (EXACT || (uint32_t)q < k) {
                     if (LSMB_ABL & 2) continue;
-                    if (FULL || pos[q] < sink) *(uint32_t*)((char*)sm + slot(q)) = pos[q] & kSliceMask;
+                    if (FULL || pos[q] < sink) *(uint32_t*)((char*)sm + slot(q)) = pos[q] & kMask;
                 }
             }
         } else {
@@ -385,9 +392,9 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
             for (int q = 0; q < NP; q++) {
                 if ((EXACT || (uint32_t)q < k) && (FULL || pos[q] < sink)) {
                     if (got[q] < lim) {
-                        *(uint32_t*)((char*)sm + slot(q)) = pos[q] & kSliceMask;
+                        *(uint32_t*)((char*)sm + slot(q)) = pos[q] & kMask;
                     } else if (pos[q] < sink) {  // (the sink's claims add 0: never past its ring)
-                        or_pos_global(a.gw, a.b0 + (pos[q] >> kSliceLog2), pos[q] & kSliceMask);
+                        or_pos_global<SL>(a.gw, a.b0 + (pos[q] >> SL), pos[q] & kMask);
 #ifdef LSMB_STATS
                         atomicAdd(a.err + 9, 1u);
 #endif
@@ -439,10 +446,10 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
             z0 = *(const uint4*)(ring + g2), z1 = *(const uint4*)(ring + g2 + 16);
         };
         auto store_segment = [&](uint32_t off) {
-            const uint2 q0 = pack3w(x0.x, y0.x, z0.x), q1 = pack3w(x0.y, y0.y, z0.y);
-            const uint2 q2 = pack3w(x0.z, y0.z, z0.z), q3 = pack3w(x0.w, y0.w, z0.w);
-            const uint2 q4 = pack3w(x1.x, y1.x, z1.x), q5 = pack3w(x1.y, y1.y, z1.y);
-            const uint2 q6 = pack3w(x1.z, y1.z, z1.z), q7 = pack3w(x1.w, y1.w, z1.w);
+            const uint2 q0 = pack3w<SL>(x0.x, y0.x, z0.x), q1 = pack3w<SL>(x0.y, y0.y, z0.y);
+            const uint2 q2 = pack3w<SL>(x0.z, y0.z, z0.z), q3 = pack3w<SL>(x0.w, y0.w, z0.w);
+            const uint2 q4 = pack3w<SL>(x1.x, y1.x, z1.x), q5 = pack3w<SL>(x1.y, y1.y, z1.y);
+            const uint2 q6 = pack3w<SL>(x1.z, y1.z, z1.z), q7 = pack3w<SL>(x1.w, y1.w, z1.w);
             if (!(LSMB_ABL & 8)) {
                 __builtin_amdgcn_raw_buffer_store_b128(u32x4{q0.x, q0.y, q1.x, q1.y}, rgn, off, 0, 0);
                 __builtin_amdgcn_raw_buffer_store_b128(u32x4{q2.x, q2.y, q3.x, q3.y}, rgn, off + 16, 0, 0);
@@ -454,7 +461,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
             const uint32_t vals[24] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w,
                                        y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w,
                                        z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
-            for (int t = 0; t < 24; t++) or_pos_global(a.gw, a.b0 + own, vals[t]);
+            for (int t = 0; t < 24; t++) or_pos_global<SL>(a.gw, a.b0 + own, vals[t]);
 #ifdef LSMB_STATS
             atomicAdd(a.err + 7, 24u);
 #endif
@@ -487,12 +494,12 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
             uint2 w0 = make_uint2(0, 0), w1 = make_uint2(0, 0);
             if (j < jobs) {
                 const uint4 jb = jobtab[wave * kBinJobsPerWave + j];
-                // segment word 2l+e = pack3(group0[2l+e], group1[2l+e], group2[2l+e])
+                // segment word 2l+e = pack3<SL>(group0[2l+e], group1[2l+e], group2[2l+e])
                 const uint2 a0 = *(const uint2*)((const char*)sm + jb.x + 8 * l);
                 const uint2 a1 = *(const uint2*)((const char*)sm + jb.y + 8 * l);
                 const uint2 a2 = *(const uint2*)((const char*)sm + jb.z + 8 * l);
-                w0 = pack3w(a0.x, a1.x, a2.x);
-                w1 = pack3w(a0.y, a1.y, a2.y);
+                w0 = pack3w<SL>(a0.x, a1.x, a2.x);
+                w1 = pack3w<SL>(a0.y, a1.y, a2.y);
                 off = (LSMB_ABL & 16) ? kDrop : jb.w + 16 * l;
             }
             if (!(LSMB_ABL & 8)) __builtin_amdgcn_raw_buffer_store_b128(u32x4{w0.x, w0.y, w1.x, w1.y}, rgn, off, 0, 0);
@@ -561,10 +568,10 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
             if (segs < a.cap) {
                 uint64_t* dst = region_ptr(a, a.b0 + own, w) + (uint64_t)segs * kSegWords;
 #pragma unroll
-                for (int t = 0; t < kSegWords; t++) dst[t] = pack3(v[t], v[t + 8], v[t + 16]);
+                for (int t = 0; t < kSegWords; t++) dst[t] = pack3<SL>(v[t], v[t + 8], v[t + 16]);
                 segs++;
             } else {
-                for (uint32_t t = 0; t < m; t++) or_pos_global(a.gw, a.b0 + own, v[t]);
+                for (uint32_t t = 0; t < m; t++) or_pos_global<SL>(a.gw, a.b0 + own, v[t]);
             }
             const uint32_t s = start + 4 * m;
             start = min(s, s - R4);
@@ -583,17 +590,35 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
 //      region's 16-B pieces are loaded U per lane at a time and every 20-bit
 //      offset is ORed into LDS;
 //   3. the slice is written back once.
+// SL = 21 (2^21-bit bins): a bin is applied as two 2^20-bit halves by two
+// workgroups, each reading all of the bin's offsets and keeping its own.
+// Units u -> (bin, half) so that the two halves of a bin are blocks u and
+// u + 8 (or u + w in a last group of w < 8 bins): the same XCD under
+// round-robin dispatch, close in time, so the second read of the bin's
+// regions mostly hits in L2 / MALL.
+template <int SL = kSliceLog2>
 __global__ __launch_bounds__(kApplyBlock) void k_apply(const uint64_t* __restrict__ regions,
                                                        const uint32_t* __restrict__ counts,
                                                        uint32_t grid, uint32_t cap, uint32_t nbins,
                                                        uint32_t* __restrict__ gw, uint64_t nw32,
                                                        uint32_t bfirst, uint32_t bend) {
+    constexpr uint32_t H = 1u << (SL - kSliceLog2);  // 2^20-bit halves per bin
+    constexpr uint32_t kMask = (1u << SL) - 1;
     __shared__ uint32_t filt[kSliceWords32];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr uint32_t NWAVE = kApplyBlock / 64;
     constexpr uint32_t PER = kSliceWords32 / 2 / kApplyBlock;  // u64 words per thread
-    for (uint32_t b = bfirst + blockIdx.x; b < bend; b += gridDim.x) {
-        const uint64_t w0 = (uint64_t)b * kSliceWords32;
+    const uint32_t nunits = (bend - bfirst) * H;
+    for (uint32_t u = blockIdx.x; u < nunits; u += gridDim.x) {
+        uint32_t b = bfirst + u, half = 0;
+        if constexpr (H > 1) {
+            const uint32_t g = u / (8 * H), r = u % (8 * H);
+            const uint32_t wdt = min(8u, bend - bfirst - g * 8);
+            b = bfirst + g * 8 + r % wdt;
+            half = r / wdt;
+        }
+        const uint64_t w0 = ((uint64_t)b * H + half) * kSliceWords32;
+        if (w0 >= nw32) continue;  // (block-uniform) the last bin's missing half
         const uint32_t nw2 = (uint32_t)min((uint64_t)kSliceWords32, nw32 - w0) / 2;  // u64 words
         uint2* g2 = reinterpret_cast<uint2*>(gw + w0);
         uint2* f2 = reinterpret_cast<uint2*>(filt);
@@ -633,10 +658,12 @@ __global__ __launch_bounds__(kApplyBlock) void k_apply(const uint64_t* __restric
                         const uint64_t hi = ((uint64_t)v[u].w << 32) | v[u].z;
 #pragma unroll
                         for (int e = 0; e < 3; e++) {
-                            const uint32_t o0 = (uint32_t)(lo >> (20 * e)) & kSliceMask;
-                            const uint32_t o1 = (uint32_t)(hi >> (20 * e)) & kSliceMask;
-                            atomicOr(&filt[o0 >> 5], 1u << (o0 & 31));
-                            atomicOr(&filt[o1 >> 5], 1u << (o1 & 31));
+                            const uint32_t o0 = (uint32_t)(lo >> (SL * e)) & kMask;
+                            const uint32_t o1 = (uint32_t)(hi >> (SL * e)) & kMask;
+                            if (H == 1 || (o0 >> kSliceLog2) == half)
+                                atomicOr(&filt[(o0 & kSliceMask) >> 5], 1u << (o0 & 31));
+                            if (H == 1 || (o1 >> kSliceLog2) == half)
+                                atomicOr(&filt[(o1 & kSliceMask) >> 5], 1u << (o1 & 31));
                         }
                     }
                 }
@@ -794,19 +821,24 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
                 kern<<<dim3(pl.grid), dim3(kBinBlock), smem, st>>>(src, n, md, k, a);
             };
             const bool full = pl.sweeps == 1;
-            if (k == 7) {
+            auto go7 = [&](auto slc) {  // k = 7 (BloomFilter::new at fpr 0.01), bin width 2^SL
+                constexpr int SL = decltype(slc)::value;
                 const bool two = pl.keys_per_lane == 2;
                 if (w32) {
-                    if (full && two) go(k_bin<Src, Walk32, 7, true, true, 2>);
-                    else if (full) go(k_bin<Src, Walk32, 7, true, true>);
-                    else if (two) go(k_bin<Src, Walk32, 7, true, false, 2>);
-                    else go(k_bin<Src, Walk32, 7, true, false>);
+                    if (full && two) go(k_bin<Src, Walk32, 7, true, true, 2, SL>);
+                    else if (full) go(k_bin<Src, Walk32, 7, true, true, 1, SL>);
+                    else if (two) go(k_bin<Src, Walk32, 7, true, false, 2, SL>);
+                    else go(k_bin<Src, Walk32, 7, true, false, 1, SL>);
                 } else {
-                    if (full && two) go(k_bin<Src, Walk64, 7, true, true, 2>);
-                    else if (full) go(k_bin<Src, Walk64, 7, true, true>);
-                    else if (two) go(k_bin<Src, Walk64, 7, true, false, 2>);
-                    else go(k_bin<Src, Walk64, 7, true, false>);
+                    if (full && two) go(k_bin<Src, Walk64, 7, true, true, 2, SL>);
+                    else if (full) go(k_bin<Src, Walk64, 7, true, true, 1, SL>);
+                    else if (two) go(k_bin<Src, Walk64, 7, true, false, 2, SL>);
+                    else go(k_bin<Src, Walk64, 7, true, false, 1, SL>);
                 }
+            };
+            if (k == 7) {
+                if (pl.slice_log2 == 21) go7(std::integral_constant<int, 21>{});
+                else go7(std::integral_constant<int, kSliceLog2>{});
             } else if (k <= 8) {
                 if (w32) go(k_bin<Src, Walk32, 8, false, false>); else go(k_bin<Src, Walk64, 8, false, false>);
             } else if (k <= 16) {
@@ -820,9 +852,15 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
         if (tm) hipEventRecord(tm->t1, st);
         const uint32_t bfirst = sweep >= 0 ? (uint32_t)sweep * pl.bins_per_sweep : 0u;
         const uint32_t bend = sweep >= 0 ? min(pl.nbins, bfirst + pl.bins_per_sweep) : pl.nbins;
-        if (bend > bfirst)
-            k_apply<<<dim3(bend - bfirst), dim3(kApplyBlock), 0, st>>>(ws.regions, ws.counts, pl.grid, pl.cap_segs,
-                                                                       pl.nbins, gw, nw32, bfirst, bend);
+        if (bend > bfirst) {
+            if (pl.slice_log2 == 21)
+                k_apply<21><<<dim3(2 * (bend - bfirst)), dim3(kApplyBlock), 0, st>>>(
+                    ws.regions, ws.counts, pl.grid, pl.cap_segs, pl.nbins, gw, nw32, bfirst, bend);
+            else
+                k_apply<<<dim3(bend - bfirst), dim3(kApplyBlock), 0, st>>>(ws.regions, ws.counts, pl.grid,
+                                                                           pl.cap_segs, pl.nbins, gw, nw32, bfirst,
+                                                                           bend);
+        }
     }
     if (tm) {
         hipEventRecord(tm->t2, st);
@@ -858,13 +896,15 @@ BuildStrategy pick_build_strategy(uint32_t num_bits, uint32_t k, uint64_t n) {
     return BuildStrategy::Partition;
 }
 
-PartitionPlan plan_partition(uint32_t num_bits, uint32_t k, uint64_t n, int num_cus) {
+namespace {
+PartitionPlan plan_partition_sl(uint32_t num_bits, uint32_t k, uint64_t n, int num_cus, uint32_t sl) {
     PartitionPlan pl;
-    pl.nbins = (uint32_t)(((uint64_t)num_bits + kSliceMask) >> kSliceLog2);
+    pl.slice_log2 = sl;
+    pl.nbins = (uint32_t)(((uint64_t)num_bits + (1ull << sl) - 1) >> sl);
     // Entries a slice's ring receives per pass A phase (1024 keys), and the
     // ring that holds a segment's worth of leftovers plus a phase's arrivals
     // with margin.  Claims past the ring fall back to exact global atomics.
-    const double lambda = (double)kBinBlock * k * fmin(1.0, (double)(1u << kSliceLog2) / (double)num_bits);
+    const double lambda = (double)kBinBlock * k * fmin(1.0, (double)(1u << sl) / (double)num_bits);
     uint32_t need = kSegEntries + (uint32_t)ceil(lambda + 2.0 * sqrt(lambda));
     need = (need + 7) & ~7u;
     if (need > kMaxRing) need = kMaxRing;
@@ -895,7 +935,7 @@ PartitionPlan plan_partition(uint32_t num_bits, uint32_t k, uint64_t n, int num_
     if (g < 1) g = 1;
     pl.grid = (uint32_t)g;
     const uint64_t keys_w = (n + g - 1) / g;  // workgroup w hashes keys [w*keys_w, (w+1)*keys_w)
-    double p = (double)(1u << kSliceLog2) / (double)num_bits;
+    double p = (double)(1u << sl) / (double)num_bits;
     if (p > 1.0) p = 1.0;
     const double mu = (double)keys_w * k * p;
     const double cap_e = mu + 8.0 * sqrt(mu) + 2.0 * kSegEntries;
@@ -907,6 +947,20 @@ PartitionPlan plan_partition(uint32_t num_bits, uint32_t k, uint64_t n, int num_
     pl.region_bytes = fits ? (uint64_t)pl.nbins * pl.grid * pl.cap_segs * 64 : ~0ull >> 2;
     pl.counts_bytes = (uint64_t)pl.nbins * pl.grid * 4;
     return pl;
+}
+}  // namespace
+
+// Bins of 2^20 bits (one pass B workgroup's LDS) unless the filter needs
+// several sweeps: then 2^21-bit bins halve the sweeps (each re-reads and
+// re-hashes every key) for a second read of each bin's regions in pass B.
+// k = 7 only (the kernels instantiated for it); LSMB_SLICE_LOG2=20 pins 2^20.
+PartitionPlan plan_partition(uint32_t num_bits, uint32_t k, uint64_t n, int num_cus) {
+    const PartitionPlan p20 = plan_partition_sl(num_bits, k, n, num_cus, kSliceLog2);
+    if (p20.sweeps < 2 || k != 7) return p20;
+    const char* e = getenv("LSMB_SLICE_LOG2");
+    if (e && atoi(e) == 20) return p20;
+    const PartitionPlan p21 = plan_partition_sl(num_bits, k, n, num_cus, 21);
+    return p21.sweeps < p20.sweeps ? p21 : p20;
 }
 
 TiledPlan plan_tiled(uint32_t num_bits, uint64_t n, int num_cus) {

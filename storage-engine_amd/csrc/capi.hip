@@ -624,7 +624,7 @@ int lsmb_sweep_words(uint32_t num_bits, uint32_t k, uint64_t n, int sweep, uint6
         return LSMB_OK;
     }
     const PartitionPlan pl = plan_partition(num_bits, k, n, 256);
-    const uint64_t w_per_slice = (1ull << kSliceLog2) / 64;
+    const uint64_t w_per_slice = (1ull << pl.slice_log2) / 64;
     *word_lo = std::min<uint64_t>(nw, (uint64_t)sweep * pl.bins_per_sweep * w_per_slice);
     *word_hi = std::min<uint64_t>(nw, ((uint64_t)sweep + 1) * pl.bins_per_sweep * w_per_slice);
     return LSMB_OK;

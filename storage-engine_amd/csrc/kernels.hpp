@@ -44,7 +44,8 @@ const char* strategy_name(BuildStrategy s);
 // its private region (b, w) as 64-B segments; pass B reads every region of
 // slice b.  No global atomics: each region has one writer.
 struct PartitionPlan {
-    uint32_t nbins = 0;           // ceil(num_bits / 2^20)
+    uint32_t slice_log2 = kSliceLog2;  // bin width: 2^20 bits, or 2^21 where that saves sweeps
+    uint32_t nbins = 0;           // ceil(num_bits / 2^slice_log2)
     uint32_t grid = 0;            // pass A workgroups = regions per slice
     uint32_t cap_segs = 0;        // region capacity, segments
     uint32_t bins_per_sweep = 0;  // slices buffered in LDS per pass A launch

@@ -164,8 +164,9 @@ def test_no_device_wide_synchronisation_in_library():
 def test_sweep_ranges_tile_the_filter():
     """lsmb_build_sweeps / lsmb_sweep_words (host-only planning): the sweeps'
     word ranges are contiguous, disjoint and cover the filter; C5's 2^32-1-bit
-    filter runs in 4 sweeps of 2^24 words, everything C2-sized in one."""
-    for filter_n, n, want in [(1_000_000_000, 125_000_000, 4), (1_000_000_000, 2_000_000, 4),
+    filter runs in 2 sweeps of 1024 2^21-bit bins (2^25 words), everything
+    C2-sized in one."""
+    for filter_n, n, want in [(1_000_000_000, 125_000_000, 2), (1_000_000_000, 2_000_000, 2),
                               (100_000_000, 100_000_000, 1), (1000, 1000, 1)]:
         nb, k = lsmbloom.params(filter_n, 0.01)
         ns = lsmbloom.build_sweeps(nb, n, k)

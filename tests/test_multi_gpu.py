@@ -98,7 +98,8 @@ def test_multi_build_fixed_dev_or_accumulates(torch, oracle):
         m.close()
 
 
-@pytest.mark.parametrize("filter_n,n", [(1_000_000_000, 2_000_000),   # C5's filter: 4 sweeps
+@pytest.mark.parametrize("filter_n,n", [(1_000_000_000, 2_000_000),   # C5's filter: 2 sweeps
+                                         (200_000_000, 2_000_000),     # 1.9e9 bits: one sweep of 2^21-bit bins
                                          (1_000_000, 1_000_000)])        # one sweep (tiled)
 def test_sweep_builds_cover_the_filter(torch, ctx, oracle, filter_n, n):
     """lsmb_build_fixed_dev_sweep: sweep s sets only the bits of its word range
@@ -111,7 +112,7 @@ def test_sweep_builds_cover_the_filter(torch, ctx, oracle, filter_n, n):
     keys = torch.from_numpy(np.ascontiguousarray(host)).to(dev)
     ref = oracle.build_fixed_mt(host, 16, nb, k, 8)
     nsw = lsmbloom.build_sweeps(nb, n, k)
-    assert nsw == (4 if filter_n == 1_000_000_000 else 1)
+    assert nsw == (2 if filter_n == 1_000_000_000 else 1)
     acc = torch.zeros(nw, dtype=torch.int64, device=dev)
     one = torch.zeros(nw, dtype=torch.int64, device=dev)
     for s in range(nsw):
@@ -217,7 +218,7 @@ def test_bench_launches_its_own_ranks(filter_keys):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
            "--global-keys", "8000000", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-e2e",
            "--no-varlen", "--no-exact10", "--probe-keys", "200000"]
-    if filter_keys:  # C5's 2^32-1-bit filter: 4 sweeps, per-range allreduce overlapped
+    if filter_keys:  # C5's 2^32-1-bit filter: 2 sweeps, per-range allreduce overlapped
         cmd += ["--filter-keys", str(filter_keys), "--no-probe"]
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
@@ -231,7 +232,7 @@ def test_bench_launches_its_own_ranks(filter_keys):
     assert out["multi_gpu_merged_equals_single_gpu_build"] is True
     assert out["step_split"]["or_allreduce_ms"] > 0 and out["step_split"]["build_ms"] > 0
     if filter_keys:
-        assert out["step_split"]["timed_step"].startswith("4 build sweeps")
+        assert out["step_split"]["timed_step"].startswith("2 build sweeps")
     assert filter_keys or out["probe"]["member_rows_all_hit"] is True
 
 
