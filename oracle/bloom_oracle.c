@@ -393,6 +393,7 @@ void oracle_gen_key16(uint64_t seed, uint64_t first, uint64_t n, uint8_t* out) {
 
 typedef struct {
     const uint8_t* keys;
+    const uint64_t* offsets; /* var-len keys when non-NULL */
     uint32_t key_len;
     uint64_t begin, end;
     uint32_t num_bits, k;
@@ -403,7 +404,10 @@ static void* mt_worker(void* arg) {
     mt_job* j = (mt_job*)arg;
     for (uint64_t i = j->begin; i < j->end; i++) {
         uint64_t h1, h2;
-        oracle_xxh3_128(j->keys + i * (uint64_t)j->key_len, j->key_len, &h1, &h2);
+        if (j->offsets)
+            oracle_xxh3_128(j->keys + j->offsets[i], j->offsets[i + 1] - j->offsets[i], &h1, &h2);
+        else
+            oracle_xxh3_128(j->keys + i * (uint64_t)j->key_len, j->key_len, &h1, &h2);
         for (uint32_t t = 0; t < j->k; t++) {
             uint32_t p = get_position(h1, h2, t, j->num_bits);
             __atomic_fetch_or(&j->words[p / 64], (uint64_t)1 << (p % 64), __ATOMIC_RELAXED);
@@ -412,14 +416,15 @@ static void* mt_worker(void* arg) {
     return NULL;
 }
 
-int oracle_bloom_build_fixed_mt(const uint8_t* keys, uint32_t key_len, uint64_t n,
-                                uint32_t num_bits, uint32_t k, uint64_t* words, int threads) {
+static int run_mt(const uint8_t* keys, const uint64_t* offsets, uint32_t key_len, uint64_t n,
+                  uint32_t num_bits, uint32_t k, uint64_t* words, int threads) {
     if (threads < 1) threads = 1;
     if (threads > 1024) threads = 1024;
     pthread_t tid[1024];
     mt_job jobs[1024];
     for (int t = 0; t < threads; t++) {
         jobs[t].keys = keys;
+        jobs[t].offsets = offsets;
         jobs[t].key_len = key_len;
         jobs[t].begin = n * (uint64_t)t / (uint64_t)threads;
         jobs[t].end = n * (uint64_t)(t + 1) / (uint64_t)threads;
@@ -430,4 +435,15 @@ int oracle_bloom_build_fixed_mt(const uint8_t* keys, uint32_t key_len, uint64_t 
     }
     for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
     return 0;
+}
+
+int oracle_bloom_build_fixed_mt(const uint8_t* keys, uint32_t key_len, uint64_t n,
+                                uint32_t num_bits, uint32_t k, uint64_t* words, int threads) {
+    return run_mt(keys, NULL, key_len, n, num_bits, k, words, threads);
+}
+
+/* oracle_bloom_build_var on `threads` threads (same bits: OR is order-independent). */
+int oracle_bloom_build_var_mt(const uint8_t* data, const uint64_t* offsets, uint64_t n,
+                              uint32_t num_bits, uint32_t k, uint64_t* words, int threads) {
+    return run_mt(data, offsets, 0, n, num_bits, k, words, threads);
 }

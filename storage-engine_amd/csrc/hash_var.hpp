@@ -38,8 +38,13 @@ struct LdsReader {
 // 0-16 / 17-128 / 129-240 / long paths otherwise (tools/mb_varhash.hip).
 // Keys that do not fit the window start another round at the first unhashed
 // key; a key longer than the whole window is hashed from global memory.
+// Occupancy is the lever (tools/mb_varhash.hip, C4 lengths): a 36 KiB window
+// and no per-key LDS arrays fit four workgroups per CU, and the kernel's 127
+// VGPRs four waves per SIMD — 3.24 ms per 1e8 keys against 3.99 ms for a 40
+// KiB window with LDS offset arrays (three workgroups, 133 VGPRs).  C4's
+// 256-key blocks average 33.8 KB (sd ~1.2 KB), so ~3 % take a second round.
 constexpr uint32_t kHashKeys = 256;       // keys (= threads) per workgroup
-constexpr uint32_t kHashWin = 40 * 1024;  // LDS window bytes
+constexpr uint32_t kHashWin = 36 * 1024;  // LDS window bytes
 
 __device__ __forceinline__ uint32_t len_class(uint64_t len) {
     if (len <= 16) return 0;
@@ -47,29 +52,24 @@ __device__ __forceinline__ uint32_t len_class(uint64_t len) {
     return 9;
 }
 
-template <int MODE = 0, uint32_t KEYS = kHashKeys, uint32_t WIN = kHashWin>
-__global__ __launch_bounds__(KEYS) void k_hash_var(const uint8_t* __restrict__ d, const uint64_t* __restrict__ o,
-                                                   uint64_t n, uint4* __restrict__ out) {
+// WPE: waves per SIMD the register allocation must allow (0: compiler's
+// choice).  The hash paths want ~130 VGPRs; at <= 128 four waves fit a SIMD.
+template <int MODE = 0, uint32_t KEYS = kHashKeys, uint32_t WIN = kHashWin, int WPE = 0>
+__global__ __launch_bounds__(KEYS) __attribute__((amdgpu_waves_per_eu(WPE ? WPE : 1)))
+void k_hash_var(const uint8_t* __restrict__ d, const uint64_t* __restrict__ o, uint64_t n, uint4* __restrict__ out) {
     constexpr uint32_t kPieces = WIN / (KEYS * 16);  // 16-B loads per thread per round
     static_assert(kPieces * KEYS * 16 == WIN, "window must be a whole number of rounds of loads");
     __shared__ uint32_t win[WIN / 4 + 8];
-    __shared__ uint64_t ks_a[KEYS], ks_b[KEYS];
     __shared__ uint32_t cls_cnt[16];
     __shared__ uint16_t perm[KEYS];
     const uint32_t t = threadIdx.x;
     const uint64_t i0 = (uint64_t)blockIdx.x * KEYS;
     const uint32_t m = (uint32_t)min<uint64_t>(KEYS, n - i0);
-    // key offsets to LDS; lane assignment by length class
-    uint64_t a0 = 0, b0 = 0;
-    if (t < m) {
-        a0 = o[i0 + t];
-        b0 = o[i0 + t + 1];
-    }
-    ks_a[t] = a0;
-    ks_b[t] = b0;
+    // lane assignment by length class (a counting sort of the block's keys)
+    uint32_t cls = 15;
+    if (t < m) cls = MODE == 2 ? 0 : len_class(o[i0 + t + 1] - o[i0 + t]);  // MODE 2 (microbenchmark): no sort
     if (t < 16) cls_cnt[t] = 0;
     __syncthreads();
-    const uint32_t cls = t < m ? len_class(b0 - a0) : 15;
     const uint32_t rank = atomicAdd(&cls_cnt[cls], 1u);
     __syncthreads();
     uint32_t base = 0;
@@ -77,7 +77,11 @@ __global__ __launch_bounds__(KEYS) void k_hash_var(const uint8_t* __restrict__ d
     perm[base + rank] = (uint16_t)t;
     __syncthreads();
     const uint32_t j = perm[t];  // the key this lane hashes
-    const uint64_t ka = ks_a[j], kb = ks_b[j];
+    uint64_t ka = 0, kb = 0;
+    if (j < m) {
+        ka = o[i0 + j];
+        kb = o[i0 + j + 1];
+    }
     const uintptr_t end = (uintptr_t)(d + o[i0 + m]);  // one past the last key byte
     const uintptr_t pa = (uintptr_t)(d + ka), pb = (uintptr_t)(d + kb);
     H128 h{0, 0};
@@ -86,7 +90,7 @@ __global__ __launch_bounds__(KEYS) void k_hash_var(const uint8_t* __restrict__ d
         // Window [A, wend): A = the 16-B block holding key f's first byte.
         // Every 16-B piece loaded holds at least one key byte, so no load
         // leaves the data's pages.
-        const uintptr_t A = (uintptr_t)(d + ks_a[f]) & ~(uintptr_t)15;
+        const uintptr_t A = (uintptr_t)(d + o[i0 + f]) & ~(uintptr_t)15;
         const uintptr_t wend = min(A + (uintptr_t)WIN, end);
         const uint32_t nb = (uint32_t)(wend - A);
         uint4 v[kPieces];

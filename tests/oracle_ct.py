@@ -44,6 +44,7 @@ def load():
         "oracle_bloom_deserialize": (I, [u8p, U64, u32p, u32p, u32p, u64p]),
         "oracle_gen_key16": (V, [U64, U64, U64, u8p]),
         "oracle_bloom_build_fixed_mt": (I, [u8p, U32, U64, U32, U32, u64p, I]),
+        "oracle_bloom_build_var_mt": (I, [u8p, u64p, U64, U32, U32, u64p, I]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -115,6 +116,16 @@ class Oracle:
             words = np.zeros(self.nwords(num_bits), dtype=np.uint64)
         self.lib.oracle_bloom_build_var(_p(data, u8p), _p(offsets, u64p), offsets.size - 1,
                                         num_bits, k, _p(words, u64p))
+        return words
+
+    def build_var_mt(self, data, offsets, num_bits, k, threads, words=None):
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        if words is None:
+            words = np.zeros(self.nwords(num_bits), dtype=np.uint64)
+        rc = self.lib.oracle_bloom_build_var_mt(_p(data, u8p), _p(offsets, u64p), offsets.size - 1,
+                                                num_bits, k, _p(words, u64p), threads)
+        assert rc == 0
         return words
 
     def insert(self, words, num_bits, k, key):

@@ -215,6 +215,24 @@ def test_build_var_c4_shape(ctx, oracle):
     _cmp(ctx.build_var(data, offs, nb, k), oracle.build_var(data, offs, nb, k))
 
 
+def test_build_var_c4_10m_exact(ctx, oracle):
+    """C4's key shape (8-256 B, tests/keygen.varlen) at 10 M keys into the
+    C4 filter new(1e8, 0.01): the device build (HBM-resident keys, the bench's
+    path) word-for-word against the multithreaded oracle."""
+    import torch
+    n = 10_000_000
+    dev = torch.device("cuda:0")
+    data_d, offs_d = ctx.gen_varlen_dev(n)
+    data, offs = data_d.cpu().numpy(), offs_d.cpu().numpy().view(np.uint64)
+    h_data, h_offs = keygen.varlen(1000)
+    assert np.array_equal(offs[:1001], h_offs) and np.array_equal(data[:int(h_offs[-1])], h_data)
+    nb, k = lsmbloom.params(100_000_000, 0.01)
+    words = torch.zeros(lsmbloom.num_words(nb), dtype=torch.int64, device=dev)
+    ctx.build_var_dev(data_d, offs_d, n, nb, k, words)
+    ref = oracle.build_var_mt(data, offs, nb, k, 16)
+    assert np.array_equal(words.cpu().numpy().view(np.uint64), ref)
+
+
 @pytest.mark.parametrize("k", [1, 2, 7, 8, 9, 16, 17, 32, 33, 40])
 def test_build_any_k(ctx, oracle, k):
     n = 200_000
@@ -390,8 +408,8 @@ def test_c4_full_size_properties(ctx, oracle):
     The monolithic build equals the OR of four shard builds (each shard's
     offsets rebased to its own data slice), sampled members probe positive
     (and agree with the host single-key path), and the fill ratio is analytic.
-    The word-exact oracle comparison of this path at smaller n is in
-    tests/test_gpu_block.py."""
+    The word-exact oracle comparison of this path at 10 M keys is
+    test_build_var_c4_10m_exact."""
     import math
 
     import torch

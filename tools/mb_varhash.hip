@@ -5,6 +5,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "hash_var.hpp"
@@ -83,6 +84,25 @@ int main(int argc, char** argv) {
         const float t_256_32 = timeit([&] { k_hash_var<0, 256, 32768><<<g, 256>>>(d, o, n, out); });
         const uint32_t g3 = (uint32_t)((n + 63) / 64);
         const float t_64_12 = timeit([&] { k_hash_var<0, 64, 12288><<<g3, 64>>>(d, o, n, out); });
+        const float t_nosort = timeit([&] { k_hash_var<2><<<g, 256>>>(d, o, n, out); });
+        const float tB = timeit([&] { k_hash_var<0, 256, 36864, 4><<<g, 256>>>(d, o, n, out); });
+        const float tC = timeit([&] { k_hash_var<0, 256, 40960, 3><<<g, 256>>>(d, o, n, out); });
+        const uint32_t g192 = (uint32_t)((n + 191) / 192);
+        const float tD = timeit([&] { k_hash_var<0, 192, 36864, 4><<<g192, 192>>>(d, o, n, out); });
+        const float tE = timeit([&] { k_hash_var<0, 128, 18432, 4><<<g2, 128>>>(d, o, n, out); });
+        const float tF = timeit([&] { k_hash_var<0, 256, 36864, 0><<<g, 256>>>(d, o, n, out); });
+        printf("   no class sort %.3f | 256/36K/w4 %.3f  256/40K/w3 %.3f  192/36K/w4 %.3f  128/18K/w4 %.3f  256/36K %.3f ms\n",
+               t_nosort, tB, tC, tD, tE, tF);
+        // k_hash_var (LDS window) vs per-lane global reads: identical records
+        std::vector<uint4> ha(n), hb(n);
+        k_hash_var<0><<<g, 256>>>(d, o, n, out);
+        CK(hipMemcpy(ha.data(), out, n * 16, hipMemcpyDeviceToHost));
+        k_hash_direct<<<g, 256>>>(d, o, n, out);
+        CK(hipMemcpy(hb.data(), out, n * 16, hipMemcpyDeviceToHost));
+        uint64_t bad = 0;
+        for (uint64_t i = 0; i < n; i++)
+            bad += ha[i].x != hb[i].x || ha[i].y != hb[i].y || ha[i].z != hb[i].z || ha[i].w != hb[i].w;
+        printf("   window vs direct mismatches %llu\n", (unsigned long long)bad);
         CK(hipDeviceSynchronize());
         printf("mode %d (%s): %.1f B/key  stage-only %.3f ms (%.0f GB/s)  lds-hash %.3f ms  direct-hash %.3f ms"
                "  | 128/20K %.3f  128/24K %.3f  256/32K %.3f  64/12K %.3f\n", mode,
