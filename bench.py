@@ -692,6 +692,37 @@ def bench_probe(ctx, dev, args, world=1, rank=0, max_over_ranks=lambda x: x):
                    "value": round(Q * world / (fms * 1e-3) / 1e6, 2), "unit": "Mkeys/s", "ms": round(fms, 4),
                    "member_rows_own_table_hit": bool(own.all().item())}
     fs.close()
+    # Mixed sizes: 4 of the C3 tables next to 4 compaction-sized ones
+    # (new(4000, 0.01), 38 271 bits): two (num_bits, k) classes, each its own
+    # bit-sliced LDS table (k_fset_classes).
+    fs = lsmbloom.FilterSet(ctx)
+    nb4, k4 = lsmbloom.params(4000, 0.01)
+    big = torch.empty((4000, 16), dtype=torch.uint8, device=dev)
+    for f in range(F):
+        if f < F // 2:
+            rows = members[f * 1000:(f + 1) * 1000].cpu().numpy()
+            bf = lsmbloom.BloomFilter(filt[f][0].cpu().numpy().view(np.uint64), k, nb)
+        else:
+            ctx.gen_key16_dev(0xF100 + f, 0, 4000, big)
+            w4 = torch.zeros(lsmbloom.num_words(nb4), dtype=torch.int64, device=dev)
+            ctx.build_fixed_dev(big, 16, 4000, nb4, k4, w4)
+            rows = big.cpu().numpy()
+            bf = lsmbloom.BloomFilter(w4.cpu().numpy().view(np.uint64), k4, nb4)
+        srt = sorted(bytes(r) for r in rows)
+        fs.add_filter(bf, srt[0], srt[-1])
+    for _ in range(max(1, args.warmup)):
+        fs.probe_dev(q, Q, fout, key_len=16)
+    torch.cuda.synchronize(dev)
+    st.record()
+    for _ in range(args.steps):
+        fs.probe_dev(q, Q, fout, key_len=16)
+    en.record()
+    torch.cuda.synchronize(dev)
+    mms = max_over_ranks(st.elapsed_time(en) / args.steps)
+    res["fset_mixed"] = {"what": "lsmb_fset_probe_dev, %d tables of two sizes: %d x new(1000, 0.01) + %d x "
+                                 "new(4000, 0.01), one LDS table per size class" % (F, F // 2, F - F // 2),
+                         "value": round(Q * world / (mms * 1e-3) / 1e6, 2), "unit": "Mkeys/s", "ms": round(mms, 4)}
+    fs.close()
     return res
 
 

@@ -354,13 +354,146 @@ __global__ __launch_bounds__(256) void k_fset_sliced(Src src, uint64_t n, const 
     }
 }
 
+// Filter-set probe over size classes (FsetClasses): a mixed set — e.g. L0
+// flush outputs new(1000, .01) next to bigger compaction outputs — keeps one
+// bit-sliced LDS table per (num_bits, k) class instead of walking every
+// filter in L2.  Per key and class with an in-range member: one walk, k
+// table reads ANDed over the class's members; the class's hits map back to
+// descriptor bits; the range mask then keeps the in-range ones.
+constexpr uint32_t kClassBlock = 1024;  // one workgroup per CU shares one copy of the tables
+
+template <class Src>
+__global__ __launch_bounds__(kClassBlock) void k_fset_classes(Src src, uint64_t n, const RangedFilter* __restrict__ filters,
+                                                      uint32_t nfilt, FsetRanges rg, FsetClasses cl,
+                                                      uint64_t* __restrict__ out) {
+    extern __shared__ __align__(16) uint8_t smem_raw[];
+    __shared__ RangedFilter fl[64];
+    __shared__ FsetLds L;
+    __shared__ FsetClass C[kFsetMaxClasses];
+    for (uint32_t f = threadIdx.x; f < nfilt; f += blockDim.x) fl[f] = filters[f];
+    for (uint32_t c = threadIdx.x; c < cl.ncls; c += blockDim.x) C[c] = cl.cls[c];
+    stage_ranges(rg, L);
+    __syncthreads();
+    // class tables: thread w builds the 32 entries of word w, 32 members a pass
+    for (uint32_t c = 0; c < cl.ncls; c++) {
+        const uint32_t nw32 = (C[c].num_bits + 31) / 32, nm = C[c].nmem, width = C[c].width;
+        uint8_t* t = smem_raw + C[c].off;
+        for (uint32_t w = threadIdx.x; w < nw32; w += blockDim.x) {
+            for (uint32_t j0 = 0; j0 < nm; j0 += 32) {
+                uint32_t acc[32];
+#pragma unroll
+                for (int b = 0; b < 32; b++) acc[b] = 0;
+                for (uint32_t j = j0; j < nm && j < j0 + 32; j++) {
+                    const uint32_t x = fl[C[c].mem[j]].f.words32[w];
+#pragma unroll
+                    for (int b = 0; b < 32; b++) acc[b] |= ((x >> b) & 1u) << (j - j0);
+                }
+#pragma unroll
+                for (int b = 0; b < 32; b++) {
+                    const uint32_t e = w * 32 + b;
+                    if (width == 1) t[e] = (uint8_t)acc[b];
+                    else if (width == 2) reinterpret_cast<uint16_t*>(t)[e] = (uint16_t)acc[b];
+                    else if (width == 4) reinterpret_cast<uint32_t*>(t)[e] = acc[b];
+                    else reinterpret_cast<uint32_t*>(t)[2 * e + (j0 >> 5)] = acc[b];
+                }
+            }
+        }
+    }
+    __syncthreads();
+    bool ident = true;  // descriptor d is output slot d
+    for (uint32_t f = 0; f < nfilt; f++) ident = ident && fl[f].f.out_bit == f;
+    const uint32_t npts = rg.npts, ncls = cl.ncls;
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
+        const H128 h = src.hash(i);
+        const uint8_t* kp = src.bytes(i);
+        const uint64_t kl = src.key_len(i);
+        const uint64_t rm = L.regmask[key_region(prefix16(kp, kl), kp, kl, L, npts)];
+        uint64_t o = 0;  // descriptor bits
+        for (uint32_t c = 0; c < ncls; c++) {
+            if (!(rm & C[c].mask)) continue;
+            const uint8_t* t = smem_raw + C[c].off;
+            const uint32_t width = C[c].width, kc = C[c].k;
+            const Mod32 md = C[c].md;
+            Walk32 pw(md, h.lo, h.hi);
+            uint64_t acc = ~0ull;
+            auto walk = [&](auto tag) {  // entry type: uniform per class
+                using E = decltype(tag);
+                const E* te = reinterpret_cast<const E*>(t);
+                if (kc == 7) {
+#pragma unroll
+                    for (int j = 0; j < 7; j++) {
+                        acc &= te[pw.pos()];
+                        if (j < 6) pw.next(md);
+                    }
+                } else {
+                    for (uint32_t j = 0; j < kc; j++) {
+                        acc &= te[pw.pos()];
+                        pw.next(md);
+                    }
+                }
+            };
+            if (width == 1) walk(uint8_t{});
+            else if (width == 2) walk(uint16_t{});
+            else if (width == 4) walk(uint32_t{});
+            else walk(uint64_t{});
+            if (C[c].nmem < 64) acc &= (1ull << C[c].nmem) - 1;
+            while (acc) {
+                const uint32_t j = (uint32_t)__builtin_ctzll(acc);
+                acc &= acc - 1;
+                o |= 1ull << C[c].mem[j];
+            }
+        }
+        uint64_t wm = rm & cl.walk_mask;
+        while (wm) {
+            const uint32_t f = (uint32_t)__builtin_ctzll(wm);
+            wm &= wm - 1;
+            const RangedFilter& R = fl[f];
+            bool hit = true;
+            if (R.f.k) {
+                PosWalk pw(R.f.md, h.lo, h.hi);
+                for (uint32_t j = 0; j < R.f.k; j++) {
+                    const uint32_t p = pw.pos();
+                    if (!((R.f.words32[p >> 5] >> (p & 31)) & 1u)) {
+                        hit = false;
+                        break;
+                    }
+                    pw.next(R.f.md);
+                }
+            }
+            if (hit) o |= 1ull << f;
+        }
+        o &= rm;
+        if (!ident) {
+            uint64_t s = 0;
+            while (o) {
+                const uint32_t d = (uint32_t)__builtin_ctzll(o);
+                o &= o - 1;
+                s |= 1ull << fl[d].f.out_bit;
+            }
+            o = s;
+        }
+        out[i] = o;
+    }
+}
+
 template <class Src>
 hipError_t fset_probe_with(const Src& src, uint64_t n, const RangedFilter* df, uint32_t nfilt, const FsetRanges& rg,
-                           uint32_t shared_nb, uint32_t shared_k, uint64_t* out, int num_cus, hipStream_t st) {
+                           const FsetClasses& cl, uint32_t shared_nb, uint32_t shared_k, uint64_t* out, int num_cus,
+                           hipStream_t st) {
     uint64_t g = (n + 255) / 256;
     const uint64_t gmax = (uint64_t)num_cus * 8;
     if (g > gmax) g = gmax;
     if (g < 1) g = 1;
+    if (!(shared_nb > 0 && shared_k > 0) && cl.ncls > 0 && cl.table_bytes <= kFsetTableBytes) {
+        const size_t smem = cl.table_bytes;
+        uint64_t gc = (n + kClassBlock - 1) / kClassBlock;
+        if (gc > (uint64_t)num_cus) gc = (uint64_t)num_cus;
+        if (gc < 1) gc = 1;
+        hipFuncSetAttribute((const void*)k_fset_classes<Src>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        k_fset_classes<Src><<<dim3((uint32_t)gc), dim3(kClassBlock), smem, st>>>(src, n, df, nfilt, rg, cl, out);
+        return hipGetLastError();
+    }
     if (shared_nb > 0 && shared_k > 0) {
         const size_t tsz = nfilt <= 8 ? 1 : nfilt <= 16 ? 2 : nfilt <= 32 ? 4 : 8;
         const size_t smem = (size_t)(((uint64_t)shared_nb + 31) / 32) * 32 * tsz;
@@ -426,15 +559,18 @@ hipError_t probe_with(const Src& src, uint64_t n, const ProbeFilter* hf, uint32_
 }  // namespace
 
 hipError_t launch_fset_probe(const KeyBatch& kb, const RangedFilter* df, uint32_t nfilt, const FsetRanges& rg,
-                             uint32_t shared_nb, uint32_t shared_k, uint64_t* out, int num_cus, hipStream_t st) {
+                             const FsetClasses& cl, uint32_t shared_nb, uint32_t shared_k, uint64_t* out, int num_cus,
+                             hipStream_t st) {
     if (kb.n == 0) return hipSuccess;
-    if (nfilt > 64 || rg.npts > kFsetMaxPoints) return hipErrorInvalidValue;
+    if (nfilt > 64 || rg.npts > kFsetMaxPoints || cl.ncls > kFsetMaxClasses) return hipErrorInvalidValue;
     if (kb.offsets)
-        return fset_probe_with(VarLen{kb.data, kb.offsets}, kb.n, df, nfilt, rg, shared_nb, shared_k, out, num_cus, st);
+        return fset_probe_with(VarLen{kb.data, kb.offsets}, kb.n, df, nfilt, rg, cl, shared_nb, shared_k, out, num_cus,
+                               st);
     if (kb.key_len == 16 && (reinterpret_cast<uintptr_t>(kb.data) & 15) == 0)
-        return fset_probe_with(Fixed16{reinterpret_cast<const uint4*>(kb.data)}, kb.n, df, nfilt, rg, shared_nb,
+        return fset_probe_with(Fixed16{reinterpret_cast<const uint4*>(kb.data)}, kb.n, df, nfilt, rg, cl, shared_nb,
                                shared_k, out, num_cus, st);
-    return fset_probe_with(FixedN{kb.data, kb.key_len}, kb.n, df, nfilt, rg, shared_nb, shared_k, out, num_cus, st);
+    return fset_probe_with(FixedN{kb.data, kb.key_len}, kb.n, df, nfilt, rg, cl, shared_nb, shared_k, out, num_cus,
+                           st);
 }
 
 hipError_t launch_probe(const KeyBatch& kb, const ProbeFilter* hf, uint32_t nfilt,

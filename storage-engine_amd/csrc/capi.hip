@@ -880,7 +880,9 @@ struct lsmb_fset {
     DevBuf ranges;  // the distinct boundary keys' bytes
     DevBuf points;  // FsetPoint[npts] then regmask[2 * npts + 1]
     DevBuf desc;    // RangedFilter[ndesc]
+    DevBuf classes; // FsetClass[cl.ncls]
     FsetRanges rg{};
+    FsetClasses cl{};
     uint32_t ndesc = 0;
     uint32_t shared_nb = 0, shared_k = 0;  // (num_bits, k) of every live slot, or 0 when they differ
     bool dirty = true;
@@ -999,7 +1001,57 @@ int fset_refresh(lsmb_fset* fs) {
     HIP_TRY(fs->desc.ensure(sizeof(RangedFilter) * 64));
     if (!d.empty())
         HIP_TRY(hipMemcpyAsync(fs->desc.p, d.data(), sizeof(RangedFilter) * d.size(), hipMemcpyHostToDevice, fs->ust));
-    HIP_TRY(hipStreamSynchronize(fs->ust));  // blob, pbuf and d are host temporaries
+    // size classes: descriptors grouped by (num_bits, k); the classes with the
+    // smallest tables go to LDS first (most filters per byte), the rest and
+    // k = 0 filters are walked from L2
+    std::vector<FsetClass> cls;
+    {
+        std::vector<std::pair<uint64_t, uint32_t>> keyd;  // (num_bits << 32 | k, descriptor)
+        for (uint32_t j = 0; j < d.size(); j++)
+            if (d[j].f.k) keyd.push_back({((uint64_t)d[j].f.num_bits << 32) | d[j].f.k, j});
+        std::sort(keyd.begin(), keyd.end());
+        std::vector<FsetClass> all;
+        for (size_t a = 0; a < keyd.size();) {
+            size_t b = a;
+            while (b < keyd.size() && keyd[b].first == keyd[a].first) b++;
+            FsetClass c;
+            memset(&c, 0, sizeof c);
+            c.num_bits = (uint32_t)(keyd[a].first >> 32);
+            c.k = (uint32_t)keyd[a].first;
+            c.md = Mod32::make(c.num_bits);
+            c.nmem = (uint32_t)(b - a);
+            c.width = c.nmem <= 8 ? 1 : c.nmem <= 16 ? 2 : c.nmem <= 32 ? 4 : 8;
+            for (size_t j = a; j < b; j++) {
+                c.mem[j - a] = (uint8_t)keyd[j].second;
+                c.mask |= 1ull << keyd[j].second;
+            }
+            all.push_back(c);
+            a = b;
+        }
+        auto tbytes = [](const FsetClass& c) { return (((uint64_t)c.num_bits + 31) / 32) * 32 * c.width; };
+        std::stable_sort(all.begin(), all.end(),
+                         [&](const FsetClass& x, const FsetClass& y) { return tbytes(x) < tbytes(y); });
+        uint64_t off = 0, in_lds = 0;
+        for (auto& c : all) {
+            const uint64_t tb = (tbytes(c) + 15) & ~15ull;
+            if (cls.size() < kFsetMaxClasses && off + tb <= kFsetTableBytes) {
+                c.off = (uint32_t)off;
+                off += tb;
+                in_lds |= c.mask;
+                cls.push_back(c);
+            }
+        }
+        uint64_t all_desc = d.size() == 64 ? ~0ull : (1ull << d.size()) - 1;
+        fs->cl.ncls = (uint32_t)cls.size();
+        fs->cl.table_bytes = (uint32_t)off;
+        fs->cl.walk_mask = all_desc & ~in_lds;
+    }
+    HIP_TRY(fs->classes.ensure(sizeof(FsetClass) * kFsetMaxClasses));
+    if (!cls.empty())
+        HIP_TRY(hipMemcpyAsync(fs->classes.p, cls.data(), sizeof(FsetClass) * cls.size(), hipMemcpyHostToDevice,
+                               fs->ust));
+    fs->cl.cls = (const FsetClass*)fs->classes.p;
+    HIP_TRY(hipStreamSynchronize(fs->ust));  // blob, pbuf, d and cls are host temporaries
     fs->ndesc = (uint32_t)d.size();
     fs->shared_nb = d.empty() ? 0 : d[0].f.num_bits;
     fs->shared_k = d.empty() ? 0 : d[0].f.k;
@@ -1062,6 +1114,7 @@ void lsmb_fset_close(lsmb_fset* fs) {
         fs->ranges.release();
         fs->points.release();
         fs->desc.release();
+        fs->classes.release();
     }
     delete fs;
 }
@@ -1110,7 +1163,7 @@ int lsmb_fset_probe_dev(lsmb_fset* fs, const void* d_data, const void* d_offsets
         return LSMB_OK;
     }
     KeyBatch kb{(const uint8_t*)d_data, (const uint64_t*)d_offsets, key_len, n};
-    HIP_TRY(launch_fset_probe(kb, (const RangedFilter*)fs->desc.p, fs->ndesc, fs->rg, fs->shared_nb, fs->shared_k,
+    HIP_TRY(launch_fset_probe(kb, (const RangedFilter*)fs->desc.p, fs->ndesc, fs->rg, fs->cl, fs->shared_nb, fs->shared_k,
                               (uint64_t*)d_out, fs->c->num_cus, st));
     return fset_note_probe(fs, st);
 }
@@ -1131,7 +1184,7 @@ int lsmb_fset_probe(lsmb_fset* fs, const uint8_t* data, const uint64_t* offsets,
         memset(out_mask, 0, n * 8);
         return LSMB_OK;
     }
-    HIP_TRY(launch_fset_probe(kb, (const RangedFilter*)fs->desc.p, fs->ndesc, fs->rg, fs->shared_nb, fs->shared_k,
+    HIP_TRY(launch_fset_probe(kb, (const RangedFilter*)fs->desc.p, fs->ndesc, fs->rg, fs->cl, fs->shared_nb, fs->shared_k,
                               (uint64_t*)c->out.p, c->num_cus, c->st));
     if (int rc = fset_note_probe(fs, c->st)) return rc;
     HIP_TRY(hipMemcpyAsync(out_mask, c->out.p, n * 8, hipMemcpyDeviceToHost, c->st));

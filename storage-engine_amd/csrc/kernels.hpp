@@ -133,12 +133,35 @@ struct FsetRanges {
     uint32_t npts;
 };
 
+// Size classes of a filter set: the live filters grouped by (num_bits, k),
+// each class a bit-sliced LDS table (entry p = its members' bit p, `width`
+// bytes), the classes together within kFsetTableBytes of LDS.  Filters of
+// classes that do not fit (and k = 0 filters) are walked from L2.
+constexpr uint32_t kFsetMaxClasses = 8;
+constexpr uint32_t kFsetTableBytes = 64 * 1024;
+struct FsetClass {
+    Mod32 md;
+    uint32_t num_bits, k;
+    uint32_t off;      // byte offset of the class table in the LDS tables
+    uint32_t width;    // entry bytes: 1, 2, 4 or 8 (members <= 8, 16, 32, 64)
+    uint32_t nmem, pad;
+    uint64_t mask;     // the members' descriptor bits
+    uint8_t mem[64];   // member j -> descriptor index
+};
+struct FsetClasses {
+    const FsetClass* cls;  // ncls, device memory
+    uint32_t ncls;
+    uint32_t table_bytes;  // LDS bytes of all class tables
+    uint64_t walk_mask;    // descriptors walked from L2
+};
+
 // out[i] bit s = (lo_s <= key i <= hi_s) && may_contain(filter s, key i), for
-// the nfilt (<= 64) descriptors at d_filters (device memory).  shared_nb /
-// shared_k: the (num_bits, k) every descriptor has, or 0 when they differ
-// (selects the bit-sliced LDS table).
+// the nfilt (<= 64) descriptors at d_filters (device memory).  One class
+// holding every descriptor takes the bit-sliced kernel with a compile-time
+// entry width; several classes the per-class tables; none the L2 walk.
 hipError_t launch_fset_probe(const KeyBatch& kb, const RangedFilter* d_filters, uint32_t nfilt, const FsetRanges& rg,
-                             uint32_t shared_nb, uint32_t shared_k, uint64_t* d_out, int num_cus, hipStream_t st);
+                             const FsetClasses& cl, uint32_t shared_nb, uint32_t shared_k, uint64_t* d_out,
+                             int num_cus, hipStream_t st);
 
 hipError_t launch_probe(const KeyBatch& kb, const ProbeFilter* h_filters, uint32_t nfilt,
                         ProbeFilter* d_filters_scratch, uint8_t* d_out, int num_cus,

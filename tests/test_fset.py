@@ -284,3 +284,36 @@ def test_fset_random_ranges_region_lookup(oracle, mixed):
     assert [int(x) for x in got] == expected_masks(oracle, tables, q)
     fs.close()
     ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sizes", [
+    [1000] * 8 + [3000] * 8 + [500] * 2,          # three classes, all in LDS tables
+    [100 * (i + 1) for i in range(11)],            # 11 classes: 8 in LDS, the rest walked
+    [1000] * 40 + [2000] * 3,                      # 40-member class (64-bit entries) + a small one
+    [1000, 200_000, 1000, 50_000, 300],            # classes too big for LDS next to small ones
+])
+def test_fset_mixed_size_classes(oracle, sizes):
+    """Mixed-size sets: one bit-sliced LDS table per (num_bits, k) class
+    (k_fset_classes), classes that do not fit walked from L2, output bits
+    mapped back to slots (slot 2 removed: a non-identity mapping)."""
+    ctx = lsmbloom.Context(0)
+    fs = FilterSet(ctx)
+    tables = {}
+    q = []
+    for t, n in enumerate(sizes):
+        keys = keygen.key16(0x5EED0700 + t, 0, min(n, 2000))
+        rows = sorted(bytes(r) for r in keys)
+        nb, k = lsmbloom.params(n, 0.01)
+        w = oracle.build_fixed(keys, 16, nb, k)
+        lo, hi = rows[t % 4 * 50], rows[-1 - t % 3 * 50]
+        s = fs.add_filter(BloomFilter(w, k, nb), lo, hi)
+        tables[s] = (w, nb, k, lo, hi)
+        q.append(keys[:300])
+    fs.remove(2)
+    del tables[2]
+    q = np.concatenate(q + [keygen.key16(0x5EED0800, 0, 5000)])
+    got = fs.probe(q, key_len=16)
+    assert [int(x) for x in got] == expected_masks(oracle, tables, [bytes(r) for r in q])
+    fs.close()
+    ctx.close()
