@@ -17,6 +17,9 @@
 //                    answer does not depend on early exit).
 //
 // Output row i (ceil(F/8) bytes): bit f%8 of byte f/8 = may_contain(f, key i).
+#include <algorithm>
+#include <type_traits>
+
 #include "kernels.hpp"
 #include "keysrc.hpp"
 
@@ -41,8 +44,11 @@ __device__ __forceinline__ void store_row(uint8_t* out, uint64_t i, uint32_t str
 // T holds up to 8*sizeof(T) filters' bits per position.
 // W: Walk32 when num_bits <= 2^31 (every intermediate fits 32 bits), else
 // Walk64.  K > 0: k fixed at compile time (7 = BloomFilter::new at fpr 0.01).
-template <class Src, typename T, class W, int K>
-__global__ __launch_bounds__(256) void k_probe_sliced(Src src, uint64_t n, Mod32 md, uint32_t k_,
+// BS: workgroup size.  The table is built once per workgroup; the hot
+// (16-B keys, 8-bit entries, k = 7) instantiations run 1024-thread
+// workgroups, two per CU, so a CU builds it twice instead of eight times.
+template <class Src, typename T, class W, int K, int BS = 256>
+__global__ __launch_bounds__(BS) void k_probe_sliced(Src src, uint64_t n, Mod32 md, uint32_t k_,
                                                       uint32_t num_bits,
                                                       const ProbeFilter* __restrict__ filters,
                                                       uint32_t nfilt, uint32_t stride,
@@ -293,8 +299,8 @@ __global__ __launch_bounds__(256) void k_fset_probe(Src src, uint64_t n, const R
 // descriptor.  A key pays one region lookup for the range checks, then k LDS
 // reads ANDed over all in-range filters at once (bits read from L2 per
 // filter in k_fset_probe).
-template <class Src, typename T, int K>
-__global__ __launch_bounds__(256) void k_fset_sliced(Src src, uint64_t n, const RangedFilter* __restrict__ filters,
+template <class Src, typename T, int K, int BS = 256>
+__global__ __launch_bounds__(BS) void k_fset_sliced(Src src, uint64_t n, const RangedFilter* __restrict__ filters,
                                                      uint32_t nfilt, FsetRanges rg, uint32_t k_,
                                                      uint64_t* __restrict__ out) {
     extern __shared__ __align__(16) uint8_t smem_raw[];
@@ -498,12 +504,15 @@ hipError_t fset_probe_with(const Src& src, uint64_t n, const RangedFilter* df, u
         const size_t tsz = nfilt <= 8 ? 1 : nfilt <= 16 ? 2 : nfilt <= 32 ? 4 : 8;
         const size_t smem = (size_t)(((uint64_t)shared_nb + 31) / 32) * 32 * tsz;
         if (smem <= 64 * 1024) {
-            auto go = [&](auto kern) {
+            auto go = [&](auto kern, uint32_t bs = 256) {
                 hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-                kern<<<dim3((uint32_t)g), dim3(256), smem, st>>>(src, n, df, nfilt, rg, shared_k, out);
+                const uint64_t gb = bs == 256 ? g : std::min<uint64_t>((n + bs - 1) / bs, 2ull * num_cus);
+                kern<<<dim3((uint32_t)std::max<uint64_t>(gb, 1)), dim3(bs), smem, st>>>(src, n, df, nfilt, rg,
+                                                                                           shared_k, out);
             };
             if (tsz == 1) {
-                if (shared_k == 7) go(k_fset_sliced<Src, uint8_t, 7>);
+                if (shared_k == 7 && std::is_same<Src, Fixed16>::value) go(k_fset_sliced<Src, uint8_t, 7, 1024>, 1024);
+                else if (shared_k == 7) go(k_fset_sliced<Src, uint8_t, 7>);
                 else go(k_fset_sliced<Src, uint8_t, 0>);
             } else if (tsz == 2) go(k_fset_sliced<Src, uint16_t, 0>);
             else if (tsz == 4) go(k_fset_sliced<Src, uint32_t, 0>);
@@ -532,14 +541,16 @@ hipError_t probe_with(const Src& src, uint64_t n, const ProbeFilter* hf, uint32_
         const size_t tsz = nfilt <= 8 ? 1 : nfilt <= 16 ? 2 : 4;
         const size_t smem = ent * tsz;
         if (smem <= 64 * 1024) {
-            auto go = [&](auto kern) {
+            auto go = [&](auto kern, uint32_t bs = 256) {
                 hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-                kern<<<dim3((uint32_t)g), dim3(256), smem, st>>>(src, n, hf[0].md, hf[0].k, nb, df, nfilt,
-                                                                 stride, out);
+                const uint64_t gb = bs == 256 ? g : std::min<uint64_t>((n + bs - 1) / bs, 2ull * num_cus);
+                kern<<<dim3((uint32_t)std::max<uint64_t>(gb, 1)), dim3(bs), smem, st>>>(src, n, hf[0].md, hf[0].k, nb,
+                                                                                           df, nfilt, stride, out);
             };
             const bool w32 = fits_walk32(nb), k7 = hf[0].k == 7;
             if (tsz == 1) {
-                if (w32 && k7) go(k_probe_sliced<Src, uint8_t, Walk32, 7>);
+                if (w32 && k7 && std::is_same<Src, Fixed16>::value) go(k_probe_sliced<Src, uint8_t, Walk32, 7, 1024>, 1024);
+                else if (w32 && k7) go(k_probe_sliced<Src, uint8_t, Walk32, 7>);
                 else if (w32) go(k_probe_sliced<Src, uint8_t, Walk32, 0>);
                 else go(k_probe_sliced<Src, uint8_t, Walk64, 0>);
             } else if (tsz == 2) {
