@@ -126,12 +126,20 @@ def test_build_partition_huge_filter(ctx, oracle):
         assert (got[:50_000] == (1 << nf) - 1).all()
 
 
-@pytest.mark.parametrize("n,filter_keys", [(24_000_000, 200_000_000), (20_000_000, 10**9)])
-def test_build_multi_sweep_steady_state(ctx, oracle, n, filter_keys):
-    # pass A sweeps (> 1024 slices): 2 sweeps at a 2-GPU run's filter, 4 at C5's
+@pytest.mark.parametrize("n,filter_keys,fpr,slice20,sweeps", [
+    (24_000_000, 200_000_000, 0.01, False, 1),   # 1825 2^20-bit slices -> one sweep of 2^21-bit bins
+    (20_000_000, 10**9, 0.01, False, 2),         # C5's filter: 2 sweeps of 2^21-bit bins
+    (20_000_000, 10**9, 0.01, True, 4),          # the same with 2^20-bit bins pinned: 4 sweeps
+    (6_000_000, 10**9, 0.001, False, 4),         # k = 10: generic-k kernels keep 2^20-bit bins
+])
+def test_build_multi_sweep_steady_state(ctx, oracle, monkeypatch, n, filter_keys, fpr, slice20, sweeps):
+    # partitioned builds of filters above 1024 bins: both bin widths, every word
+    if slice20:
+        monkeypatch.setenv("LSMB_SLICE_LOG2", "20")
     keys = keygen.key16(0x5EED0001, 0, n)
-    nb, k = lsmbloom.params(filter_keys, 0.01)
-    assert lsmbloom.build_strategy(nb, n) == "partition"
+    nb, k = lsmbloom.params(filter_keys, fpr)
+    assert lsmbloom.build_strategy(nb, n, k) == "partition"
+    assert lsmbloom.build_sweeps(nb, n, k) == sweeps
     _cmp(ctx.build_fixed(keys, 16, nb, k), oracle.build_fixed_mt(keys, 16, nb, k, 16))
 
 

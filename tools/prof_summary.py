@@ -32,7 +32,7 @@ def traffic_json(d, out):
             per[kn][cn] = sum(v) / len(v)
     kern = {}
     for kn, m in per.items():
-        if kn.startswith("k_bin<ks::Fixed16") or kn == "k_apply":
+        if kn.startswith("k_bin<ks::Fixed16") or kn.startswith("k_apply"):
             kern[kn] = {"read_bytes": int(2 * m.get("FETCH_SIZE", 0) * 1024),
                         "write_bytes": int(m.get("WRITE_SIZE", 0) * 1024)}
     tot = sum(v["read_bytes"] + v["write_bytes"] for v in kern.values())
