@@ -80,6 +80,7 @@ hipError_t launch_or_gather(uint64_t* dst, const OrSources& s, uint64_t nwords, 
 
 struct lsmb_multi {
     std::vector<lsmb_ctx*> ctx;  // one per shard
+    std::vector<hipStream_t> mst;                 // per shard: merge stream (device builds overlap it)
     std::vector<hipEvent_t> ev_built, ev_merged;  // per shard, recorded on the shard's stream
     std::vector<hipEvent_t> t0, t1, t2;           // timing per shard: start, built, merged
     std::vector<DevBuf> words;                    // per-shard device words (host-key builds)
@@ -126,43 +127,53 @@ int for_shards(lsmb_multi* m, F&& f) {
     return LSMB_OK;
 }
 
-// Reduce-scatter: after every shard's build (ev_built), shard g ORs slice g of
-// all partials into its own partial.  `part[j]` = shard j's words (device of j).
-int merge_reduce_scatter(lsmb_multi* m, uint64_t* const* part, uint64_t nw) {
+// The stream shard g merges on: its build stream, or (overlapped device
+// builds) its merge stream.
+hipStream_t merge_stream(lsmb_multi* m, int g, bool side) { return side ? m->mst[g] : m->ctx[g]->st; }
+
+// Reduce-scatter of words [base, base + nw): after every shard's build
+// (ev_built), shard g ORs sub-slice g of all partials into its own partial.
+// `part[j]` = shard j's words (device of j).
+int merge_reduce_scatter(lsmb_multi* m, uint64_t* const* part, uint64_t nw, uint64_t base = 0, bool side = false) {
     const int G = shards(m);
     for (int g = 0; g < G; g++) {
         lsmb_ctx* c = m->ctx[g];
         DevGuard dg(c->dev);
+        const hipStream_t st = merge_stream(m, g, side);
         for (int j = 0; j < G; j++)
-            if (j != g) HIP_TRY(hipStreamWaitEvent(c->st, m->ev_built[j], 0));
+            if (j != g || side) HIP_TRY(hipStreamWaitEvent(st, m->ev_built[j], 0));
         uint64_t lo, hi;
         slice_of(nw, G, g, &lo, &hi);
+        lo += base, hi += base;
         OrSources s;
         s.n = (uint32_t)G;
         for (int j = 0; j < G; j++) s.p[j] = part[j] + lo;
-        HIP_TRY(launch_or_gather(part[g] + lo, s, hi - lo, c->num_cus, c->st));
-        HIP_TRY(hipEventRecord(m->ev_merged[g], c->st));
+        HIP_TRY(launch_or_gather(part[g] + lo, s, hi - lo, c->num_cus, st));
+        HIP_TRY(hipEventRecord(m->ev_merged[g], st));
     }
     return LSMB_OK;
 }
 
-// All-gather: shard g copies every other shard's merged slice into its words.
-int merge_all_gather(lsmb_multi* m, uint64_t* const* part, uint64_t nw) {
+// All-gather of words [base, base + nw): shard g copies every other shard's
+// merged sub-slice into its words.
+int merge_all_gather(lsmb_multi* m, uint64_t* const* part, uint64_t nw, uint64_t base = 0, bool side = false) {
     const int G = shards(m);
     for (int g = 0; g < G; g++) {
         lsmb_ctx* c = m->ctx[g];
         DevGuard dg(c->dev);
+        const hipStream_t st = merge_stream(m, g, side);
         for (int j = 0; j < G; j++) {
             if (j == g) continue;
-            HIP_TRY(hipStreamWaitEvent(c->st, m->ev_merged[j], 0));
+            HIP_TRY(hipStreamWaitEvent(st, m->ev_merged[j], 0));
             uint64_t lo, hi;
             slice_of(nw, G, j, &lo, &hi);
+            lo += base, hi += base;
             if (hi == lo) continue;
             const int dj = m->ctx[j]->dev;
             if (dj == c->dev)
-                HIP_TRY(hipMemcpyAsync(part[g] + lo, part[j] + lo, (hi - lo) * 8, hipMemcpyDeviceToDevice, c->st));
+                HIP_TRY(hipMemcpyAsync(part[g] + lo, part[j] + lo, (hi - lo) * 8, hipMemcpyDeviceToDevice, st));
             else
-                HIP_TRY(hipMemcpyPeerAsync(part[g] + lo, c->dev, part[j] + lo, dj, (hi - lo) * 8, c->st));
+                HIP_TRY(hipMemcpyPeerAsync(part[g] + lo, c->dev, part[j] + lo, dj, (hi - lo) * 8, st));
         }
     }
     return LSMB_OK;
@@ -215,6 +226,11 @@ int lsmb_multi_open(lsmb_multi** out, const int* devices, int ndev) {
                 return hip_fail(e, "hipDeviceEnablePeerAccess");
             }
         }
+        m->mst.push_back(nullptr);
+        if (hipStreamCreateWithFlags(&m->mst[g], hipStreamNonBlocking) != hipSuccess) {
+            lsmb_multi_close(m);
+            return fail(LSMB_EHIP, "merge stream creation failed on device %d", m->ctx[g]->dev);
+        }
         m->ev_built.push_back(nullptr);
         m->ev_merged.push_back(nullptr);
         m->t0.push_back(nullptr);
@@ -238,6 +254,7 @@ void lsmb_multi_close(lsmb_multi* m) {
     for (size_t g = 0; g < m->ctx.size(); g++) {
         DevGuard dg(m->ctx[g]->dev);
         hipStreamSynchronize(m->ctx[g]->st);
+        if (g < m->mst.size() && m->mst[g]) hipStreamSynchronize(m->mst[g]), hipStreamDestroy(m->mst[g]);
         for (auto* v : {&m->ev_built, &m->ev_merged, &m->t0, &m->t1, &m->t2})
             if (g < v->size() && (*v)[g]) hipEventDestroy((*v)[g]);
         if (g < m->words.size()) m->words[g].release();
@@ -261,28 +278,46 @@ int lsmb_multi_build_fixed_dev(lsmb_multi* m, const void* const* d_keys, const u
     const uint64_t nw = nwords64(num_bits);
     for (int g = 0; g < G; g++)
         if (!d_words[g] || (n[g] && !d_keys[g])) return fail(LSMB_EINVAL, "null device pointer (shard %d)", g);
-    // 1. every shard's partial build, enqueued on its own stream (asynchronous)
+    // Partitioned builds of big filters run in sweeps (lsmb_build_sweeps); sweep
+    // s completes one word range.  Per sweep: every shard builds it on its
+    // build stream (asynchronous), then the range is reduce-scattered and
+    // all-gathered on the shards' merge streams while sweep s + 1 builds.
+    uint64_t nmax = 0;
+    for (int g = 0; g < G; g++) nmax = std::max(nmax, n[g]);
+    const int nsw = (G > 1 && k) ? lsmb_build_sweeps(num_bits, k, nmax) : 1;
+    std::vector<uint64_t*> part(G);
+    for (int g = 0; g < G; g++) part[g] = (uint64_t*)d_words[g];
+    for (int g = 0; g < G; g++) {
+        DevGuard dg(m->ctx[g]->dev);
+        HIP_TRY(hipEventRecord(m->t0[g], m->ctx[g]->st));
+    }
+    for (int sw = 0; sw < nsw; sw++) {
+        for (int g = 0; g < G; g++) {
+            lsmb_ctx* c = m->ctx[g];
+            DevGuard dg(c->dev);
+            if (n[g] && k) {
+                KeyBatch kb{(const uint8_t*)d_keys[g], nullptr, key_len, key_len ? n[g] : 1};
+                if (int rc = build_dev(c, kb, num_bits, k, (uint32_t*)d_words[g], c->st, nsw > 1 ? sw : -1)) return rc;
+            }
+            if (sw + 1 == nsw) HIP_TRY(hipEventRecord(m->t1[g], c->st));
+            HIP_TRY(hipEventRecord(m->ev_built[g], c->st));
+        }
+        if (G > 1) {
+            uint64_t lo = 0, hi = nw;
+            if (nsw > 1 && lsmb_sweep_words(num_bits, k, nmax, sw, &lo, &hi)) return LSMB_EINVAL;
+            const bool side = nsw > 1;
+            if (int rc = merge_reduce_scatter(m, part.data(), hi - lo, lo, side)) return rc;
+            if (int rc = merge_all_gather(m, part.data(), hi - lo, lo, side)) return rc;
+        }
+    }
     for (int g = 0; g < G; g++) {
         lsmb_ctx* c = m->ctx[g];
         DevGuard dg(c->dev);
-        HIP_TRY(hipEventRecord(m->t0[g], c->st));
-        if (n[g] && k) {
-            KeyBatch kb{(const uint8_t*)d_keys[g], nullptr, key_len, key_len ? n[g] : 1};
-            if (int rc = build_dev(c, kb, num_bits, k, (uint32_t*)d_words[g], c->st)) return rc;
+        if (nsw > 1 && G > 1) {  // the build stream takes the merges back: callers sync on it
+            HIP_TRY(hipEventRecord(m->ev_merged[g], m->mst[g]));
+            HIP_TRY(hipStreamWaitEvent(c->st, m->ev_merged[g], 0));
         }
-        HIP_TRY(hipEventRecord(m->t1[g], c->st));
-        HIP_TRY(hipEventRecord(m->ev_built[g], c->st));
-    }
-    // 2. OR reduce-scatter by peer loads, 3. all-gather
-    std::vector<uint64_t*> part(G);
-    for (int g = 0; g < G; g++) part[g] = (uint64_t*)d_words[g];
-    if (G > 1) {
-        if (int rc = merge_reduce_scatter(m, part.data(), nw)) return rc;
-        if (int rc = merge_all_gather(m, part.data(), nw)) return rc;
-    }
-    for (int g = 0; g < G; g++) {
-        DevGuard dg(m->ctx[g]->dev);
-        HIP_TRY(hipEventRecord(m->t2[g], m->ctx[g]->st));
+        HIP_TRY(hipEventRecord(m->t2[g], c->st));
     }
     m->timed = true;
     return sync_all(m);

@@ -53,6 +53,8 @@ def _u64(t):
 
 
 @pytest.mark.parametrize("G,n,filter_n", [(2, 2_000_000, 50_000_000),   # partition
+                                          (2, 2_000_000, 10**9),        # 2 sweeps: merge overlapped per range
+                                          (3, 600_001, 10**9),          # 2 sweeps, ragged shards
                                           (3, 1_000_001, 1_000_000),    # tiled, ragged shards
                                           (4, 40_000, 40_000),          # lds, odd word count
                                           (2, 3, 10_000_000)])          # atomic, shards of 1-2 keys
