@@ -384,6 +384,14 @@ def main():
                 out["multi_gpu_check_error"] = repr(e)[:200]
         dist.barrier()
 
+    # Full-size parity in the bench line itself: the filter the timed steps built
+    # (N = 1: C2; N > 1: the merged C5 filter on rank 0) against the oracle's
+    # committed digest.  Outside the timed region.
+    if rank == 0 and not args.filter_keys and scaling == "strong":
+        name = {100_000_000: "c2", 1_000_000_000: "c5"}.get(total)
+        if name:
+            torch.cuda.synchronize(dev)
+            out["words_equal_oracle_fixture"] = fixture_check(words, name, nb)
     if args.verify and rank == 0 and world == 1:
         import oracle_ct
         orc = oracle_ct.load()
@@ -453,6 +461,8 @@ def bench_exact10(ctx, keys, n, reps=10):
     # expected fill of an ideal filter: 1 - exp(-k n / m)
     res["fill_ratio"] = round(fill / nb, 5)
     res["fill_ratio_expected"] = round(1 - float(np.exp(-k * n / nb)), 5)
+    if n == 100_000_000:
+        res["words_equal_oracle_fixture"] = fixture_check(w, "c2_exact10", nb)
     del w
     return res
 
@@ -589,6 +599,8 @@ def bench_varlen(ctx, dev, args):
            "achieved_GBs": round(alg / (kt[0] * 1e-3) / 1e9, 1),
            "frac": round(alg / (kt[0] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
            "strategy": lsmbloom.build_strategy(nb, n)}
+    if n == 100_000_000:
+        res["words_equal_oracle_fixture"] = fixture_check(words, "c4", nb)
     del data, offs, words
     torch.cuda.empty_cache()
     return res
@@ -621,6 +633,25 @@ def committed_traffic():
     t = json.load(open(p))
     return {"bytes": t.get("build_bytes"), "source": "%s (%s)" % (os.path.relpath(p, ROOT), t.get("profile")),
             "fresh": t.get("kernel_src_sha") == build_sources_sha()}
+
+
+def fixture_check(words, name, num_bits):
+    """Every word of a full-size filter against the oracle's digest committed in
+    tests/golden/fullsize_fixture.json (tests/golden/gen_fullsize.py): True /
+    False, or None when this run's configuration is not the fixture's."""
+    import hashlib
+    import json
+
+    import numpy as np
+    p = os.path.join(ROOT, "tests", "golden", "fullsize_fixture.json")
+    if not os.path.exists(p):
+        return None
+    fx = json.load(open(p)).get(name)
+    if not fx or fx["num_bits"] != num_bits:
+        return None
+    w = np.ascontiguousarray(words.cpu().numpy().view(np.uint64), dtype="<u8")
+    return bool(w.size == fx["words"] and int(np.bitwise_count(w).sum()) == fx["popcount"]
+                and hashlib.sha256(w.tobytes()).hexdigest() == fx["sha256"])
 
 
 def bench_probe(ctx, dev, args, world=1, rank=0, max_over_ranks=lambda x: x):

@@ -486,7 +486,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
         // (the job table is this wave's own: its LDS writes and reads stay in order)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         // 2. kCoopRounds store instructions: lane L writes 16 B of job r*16 + L/4
-        constexpr uint32_t kCoopRounds = kBinJobsPerWave / 16;
+        constexpr uint32_t kCoopRounds = (kBinJobsPerWave + 15) / 16;
 #pragma unroll
         for (uint32_t r = 0; r < kCoopRounds; r++) {
             const uint32_t j = r * 16 + (lane >> 2), l = lane & 3;

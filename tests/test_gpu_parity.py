@@ -23,6 +23,19 @@ GOLD = os.path.join(ROOT, "tests", "golden")
 KATS = json.load(open(os.path.join(GOLD, "bloom_kats.json")))
 C1 = json.load(open(os.path.join(GOLD, "c1_fixture.json")))
 VAR = json.load(open(os.path.join(GOLD, "varlen_fixture.json")))
+FULL = json.load(open(os.path.join(GOLD, "fullsize_fixture.json")))  # tests/golden/gen_fullsize.py
+
+
+def assert_full_fixture(host_words, name):
+    """The GPU's full-size filter == the oracle's (digest committed in
+    tests/golden/fullsize_fixture.json): popcount, first/last words, sha256."""
+    import hashlib
+    fx = FULL[name]
+    w = np.ascontiguousarray(host_words, dtype="<u8")
+    assert w.size == fx["words"]
+    assert [int(x) for x in w[:8]] == fx["first8"] and [int(x) for x in w[-8:]] == fx["last8"], name
+    assert int(np.bitwise_count(w).sum()) == fx["popcount"], name
+    assert hashlib.sha256(w.tobytes()).hexdigest() == fx["sha256"], name
 
 
 @pytest.fixture(scope="module")
@@ -364,6 +377,21 @@ def test_c2_full_size_bit_exact(ctx, oracle):
     host = oracle.key16(0x5EED0001, 0, n)
     ref = oracle.build_fixed_mt(host, 16, nb, k, 16)
     _cmp(got, ref)
+    assert_full_fixture(got, "c2")
+
+
+def test_c2_exact10_full_size_fixture(ctx):
+    """C2's exact 10 bits/key variant (num_bits = 1e9, k = 7):
+    100 M key16 on the device, every word against the oracle's digest."""
+    import torch
+    n = 100_000_000
+    dev = torch.device("cuda:0")
+    keys = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+    ctx.gen_key16_dev(0x5EED0001, 0, n, keys)
+    words = torch.zeros(lsmbloom.num_words(10 * n), dtype=torch.int64, device=dev)
+    ctx.build_fixed_dev(keys, 16, n, 10 * n, 7, words)
+    torch.cuda.synchronize()
+    assert_full_fixture(words.cpu().numpy().view(np.uint64), "c2_exact10")
 
 
 def test_c5_full_size_shards_or_equal_monolithic(ctx):
@@ -372,8 +400,8 @@ def test_c5_full_size_shards_or_equal_monolithic(ctx):
     with the native OR-reduce must equal the monolithic build of all 1e9 keys
     (OR is associative, commutative and idempotent), every sampled member must
     probe positive, and the fill ratio must match 1 - exp(-kN/m).  These are
-    size-independent properties; the word-exact oracle comparison for this
-    filter is test_build_multi_sweep_steady_state."""
+    size-independent properties, and the monolithic filter's digest equals
+    the oracle's full-size C5 filter (tests/golden/fullsize_fixture.json)."""
     import math
 
     import torch
@@ -397,6 +425,7 @@ def test_c5_full_size_shards_or_equal_monolithic(ctx):
     assert torch.equal(merged, mono)
     del parts, merged
     host_words = mono.cpu().numpy().view(np.uint64)
+    assert_full_fixture(host_words, "c5")  # every word == the oracle's C5 filter
     ones = int(np.unpackbits(host_words.view(np.uint8)).sum())
     assert abs(ones / nb - (1 - math.exp(-k * N / nb))) < 1e-3, ones / nb
     sample = keys[::1_000_003][:1000].contiguous()
@@ -452,6 +481,7 @@ def test_c4_full_size_properties(ctx, oracle):
     assert torch.equal(merged, mono)
     del merged
     host_words = mono.cpu().numpy().view(np.uint64)
+    assert_full_fixture(host_words, "c4")  # every word == the oracle's C4 filter
     ones = int(np.bitwise_count(host_words).sum(dtype=np.uint64))
     tick("fill counted")
     assert abs(ones / nb - (1 - math.exp(-k * N / nb))) < 1e-3, ones / nb
