@@ -17,6 +17,8 @@
 //                    answer does not depend on early exit).
 //
 // Output row i (ceil(F/8) bytes): bit f%8 of byte f/8 = may_contain(f, key i).
+#include <stdlib.h>
+
 #include <algorithm>
 #include <type_traits>
 
@@ -483,6 +485,17 @@ __global__ __launch_bounds__(kClassBlock) void k_fset_classes(Src src, uint64_t 
     }
 }
 
+// 1024-thread sliced-probe workgroups per CU: measured best 1 for the probe
+// (0.0625 vs 0.0648 ms at 2) and 2 for the filter set (0.082 vs 0.093 at 1);
+// LSMB_PROBE_WGS_PER_CU overrides both (measurement knob, tools/probe_wgs.sh).
+uint64_t probe_wgs_per_cu(uint64_t dflt) {
+    static const long v = [] {
+        const char* e = getenv("LSMB_PROBE_WGS_PER_CU");
+        return e ? atol(e) : 0L;
+    }();
+    return v >= 1 && v <= 8 ? (uint64_t)v : dflt;
+}
+
 template <class Src>
 hipError_t fset_probe_with(const Src& src, uint64_t n, const RangedFilter* df, uint32_t nfilt, const FsetRanges& rg,
                            const FsetClasses& cl, uint32_t shared_nb, uint32_t shared_k, uint64_t* out, int num_cus,
@@ -506,7 +519,7 @@ hipError_t fset_probe_with(const Src& src, uint64_t n, const RangedFilter* df, u
         if (smem <= 64 * 1024) {
             auto go = [&](auto kern, uint32_t bs = 256) {
                 hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-                const uint64_t gb = bs == 256 ? g : std::min<uint64_t>((n + bs - 1) / bs, 2ull * num_cus);
+                const uint64_t gb = bs == 256 ? g : std::min<uint64_t>((n + bs - 1) / bs, probe_wgs_per_cu(2) * num_cus);
                 kern<<<dim3((uint32_t)std::max<uint64_t>(gb, 1)), dim3(bs), smem, st>>>(src, n, df, nfilt, rg,
                                                                                            shared_k, out);
             };
@@ -543,7 +556,7 @@ hipError_t probe_with(const Src& src, uint64_t n, const ProbeFilter* hf, uint32_
         if (smem <= 64 * 1024) {
             auto go = [&](auto kern, uint32_t bs = 256) {
                 hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-                const uint64_t gb = bs == 256 ? g : std::min<uint64_t>((n + bs - 1) / bs, 2ull * num_cus);
+                const uint64_t gb = bs == 256 ? g : std::min<uint64_t>((n + bs - 1) / bs, probe_wgs_per_cu(1) * num_cus);
                 kern<<<dim3((uint32_t)std::max<uint64_t>(gb, 1)), dim3(bs), smem, st>>>(src, n, hf[0].md, hf[0].k, nb,
                                                                                            df, nfilt, stride, out);
             };
