@@ -928,9 +928,19 @@ PartitionPlan plan_partition_sl(uint32_t num_bits, uint32_t k, uint64_t n, int n
         const uint32_t need2 = (kSegEntries + (uint32_t)ceil(2 * lambda + 2.0 * sqrt(2 * lambda)) + 7) & ~7u;
         if ((pl.ring >= need2 && !(e && atoi(e) == 1)) || (e && atoi(e) == 2)) pl.keys_per_lane = 2;
     }
-    // one 1024-thread workgroup per CU, at least ~kBinBlock keys each
+    // 1024-thread workgroups (one resident per CU), at least ~kBinBlock keys
+    // each: two per CU for 2^20-bit bins — pass B then streams twice as many,
+    // half-size regions per slice (C2: pass B 0.448 -> 0.411 ms, pass A
+    // unchanged) — one for 2^21-bit bins, whose two half-bin workgroups each
+    // read every region (C5 shard: pass B 0.843 -> 0.986 ms at two).
+    // LSMB_BIN_WGS_PER_CU overrides (measurement knob, tools/bin_wgs.sh).
     const uint64_t gmax = (n + kBinBlock - 1) / kBinBlock;
-    uint64_t g = (uint64_t)num_cus;
+    static const long wenv = [] {
+        const char* e = getenv("LSMB_BIN_WGS_PER_CU");
+        return e ? atol(e) : 0L;
+    }();
+    const uint64_t wpc = wenv >= 1 && wenv <= 4 ? (uint64_t)wenv : (sl == kSliceLog2 ? 2 : 1);
+    uint64_t g = (uint64_t)num_cus * wpc;
     if (g > gmax) g = gmax;
     if (g < 1) g = 1;
     pl.grid = (uint32_t)g;
