@@ -251,8 +251,8 @@ def main():
     side = torch.cuda.Stream(dev) if overlap else None
     sweep_ev = [torch.cuda.Event() for _ in range(nsw)]
 
-    def step():
-        if not overlap:
+    def step(ov=None):
+        if not (overlap if ov is None else ov):
             build()
             allreduce()
             return
@@ -282,6 +282,24 @@ def main():
     for _ in range(args.warmup):
         step()
     barrier()
+    calib = None
+    if overlap:
+        # The overlapped collective shares the CUs with pass A, whose workgroups
+        # each need a whole CU's LDS: whether the overlap pays depends on the
+        # node.  Time a few steps each way (untimed for the metric; the max over
+        # ranks, so every rank picks the same) and time the faster form.
+        def timed(ov, reps):
+            barrier()
+            t = time.perf_counter()
+            for _ in range(reps):
+                step(ov)
+            barrier()
+            return max_over_ranks(time.perf_counter() - t) / reps * 1e3
+        reps = max(2, min(5, args.steps))
+        t_ov, t_ser = timed(True, reps), timed(False, reps)
+        overlap = t_ov <= t_ser
+        calib = {"overlapped_ms_per_step": round(t_ov, 4), "serial_ms_per_step": round(t_ser, 4),
+                 "steps_each": reps, "timed_form": "overlapped" if overlap else "serial"}
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -349,6 +367,7 @@ def main():
                                      "bitwise-OR allreduce (all_to_all reduce-scatter + native OR kernel "
                                      "+ all_gather) of the whole filter",
                              "serial_ms_per_step": round(serial_ms, 4),
+                             "overlap_calibration": calib,
                              "timed_step": ("%d build sweeps, each sweep's word range OR-allreduced on a side "
                                             "stream while the next sweep builds" % nsw) if overlap
                                            else "build then OR-allreduce",

@@ -233,8 +233,10 @@ def test_bench_launches_its_own_ranks(filter_keys):
     assert out["scaling"] == "strong" and out["config"]["keys_per_gpu"] == 4_000_000
     assert out["multi_gpu_merged_equals_single_gpu_build"] is True
     assert out["step_split"]["or_allreduce_ms"] > 0 and out["step_split"]["build_ms"] > 0
-    if filter_keys:
-        assert out["step_split"]["timed_step"].startswith("2 build sweeps")
+    if filter_keys:  # overlapped vs serial steps timed first; the faster form is the timed one
+        cal = out["step_split"]["overlap_calibration"]
+        assert cal["overlapped_ms_per_step"] > 0 and cal["serial_ms_per_step"] > 0
+        assert out["step_split"]["timed_step"].startswith("2 build sweeps") == (cal["timed_form"] == "overlapped")
     assert filter_keys or out["probe"]["member_rows_all_hit"] is True
 
 
