@@ -963,11 +963,14 @@ PartitionPlan plan_partition_sl(uint32_t num_bits, uint32_t k, uint64_t n, int n
 // Bins of 2^20 bits (one pass B workgroup's LDS) unless the filter needs
 // several sweeps: then 2^21-bit bins halve the sweeps (each re-reads and
 // re-hashes every key) for a second read of each bin's regions in pass B.
-// k = 7 only (the kernels instantiated for it); LSMB_SLICE_LOG2=20 pins 2^20.
+// k = 7 only (the kernels instantiated for it); LSMB_SLICE_LOG2=20 pins 2^20,
+// =21 forces 2^21 (measurement knobs).
 PartitionPlan plan_partition(uint32_t num_bits, uint32_t k, uint64_t n, int num_cus) {
     const PartitionPlan p20 = plan_partition_sl(num_bits, k, n, num_cus, kSliceLog2);
-    if (p20.sweeps < 2 || k != 7) return p20;
     const char* e = getenv("LSMB_SLICE_LOG2");
+    if (k == 7 && e && atoi(e) == 21 && num_bits > (1u << 21))  // measurement: force 2^21-bit bins
+        return plan_partition_sl(num_bits, k, n, num_cus, 21);
+    if (p20.sweeps < 2 || k != 7) return p20;
     if (e && atoi(e) == 20) return p20;
     const PartitionPlan p21 = plan_partition_sl(num_bits, k, n, num_cus, 21);
     return p21.sweeps < p20.sweeps ? p21 : p20;
