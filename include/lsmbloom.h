@@ -215,6 +215,23 @@ int lsmb_sweep_words(uint32_t num_bits, uint32_t num_hashes, uint64_t n, int swe
 int lsmb_build_fixed_dev_sweep(lsmb_ctx* ctx, const void* d_keys, uint32_t key_len, uint64_t n,
                                uint32_t num_bits, uint32_t num_hashes, void* d_words, int sweep, void* stream);
 
+/* CRC-32 of bloom blocks (optional checksum; the reference's
+ * bloom block has none).  The same CRC as crc32fast::hash / zlib.crc32, which
+ * the store already uses for WAL records and the manifest
+ * (src/wal/record.rs:96,122, src/manifest/mod.rs:5).
+ *   lsmb_crc32          host bytes, appended to crc (0 to start)
+ *   lsmb_crc32_combine  CRC(A||B) from CRC(A), CRC(B), |B|
+ *   lsmb_crc32_dev      device bytes (parallel CRC + combine), appended to crc
+ *   lsmb_build_block_crc  lsmb_build_block + the block's CRC-32, the words'
+ *                         part computed on the device copy before the D2H
+ *   lsmb_fset_add_crc   lsmb_fset_add that checks the block's CRC-32 on the
+ *                       copy in HBM: mismatch -> LSMB_ECORRUPT, slot not added */
+uint32_t lsmb_crc32(uint32_t crc, const uint8_t* data, uint64_t len);
+uint32_t lsmb_crc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
+int lsmb_crc32_dev(lsmb_ctx* ctx, uint32_t crc, const void* d_data, uint64_t len, uint32_t* out, void* stream);
+int lsmb_build_block_crc(lsmb_ctx* ctx, const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
+                         uint32_t num_bits, uint32_t num_hashes, uint8_t* block, uint64_t block_len, uint32_t* crc);
+
 /* d_filt_words: host array of nfilt DEVICE pointers. */
 int lsmb_probe_dev(lsmb_ctx* ctx, const void* const* d_filt_words, const uint32_t* filt_bits,
                    const uint32_t* filt_hashes, uint32_t nfilt, const void* d_data,
@@ -303,6 +320,11 @@ void lsmb_fset_close(lsmb_fset* fs);
  * Returns the filter's slot (0..63, bit `slot` of the probe mask) or < 0. */
 int lsmb_fset_add(lsmb_fset* fs, const uint8_t* block, uint64_t len, const uint8_t* min_key,
                   uint64_t min_len, const uint8_t* max_key, uint64_t max_len);
+
+/* lsmb_fset_add that also checks the block's CRC-32 (lsmb_crc32 /
+ * crc32fast::hash of all `len` bytes) on the copy in device memory. */
+int lsmb_fset_add_crc(lsmb_fset* fs, const uint8_t* block, uint64_t len, uint32_t crc, const uint8_t* min_key,
+                      uint64_t min_len, const uint8_t* max_key, uint64_t max_len);
 
 /* Same from in-memory filter words (ceil(num_bits/64) LE u64). */
 int lsmb_fset_add_words(lsmb_fset* fs, const uint64_t* words, uint32_t num_bits, uint32_t num_hashes,

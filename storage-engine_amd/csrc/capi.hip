@@ -337,13 +337,18 @@ int host_build_dev(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, ui
     return LSMB_OK;
 }
 
+// crc (optional): CRC-32 of the words appended to *crc (the CRC of the bytes
+// before them), computed on the device copy for device builds.
 int host_build(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
-               uint32_t num_bits, uint32_t k, const uint64_t* words_in, uint8_t* words_out) {
+               uint32_t num_bits, uint32_t k, const uint64_t* words_in, uint8_t* words_out, uint32_t* crc = nullptr) {
     const uint64_t nw = nwords64(num_bits);
     {
         const uint64_t kb = offsets ? offsets[n] - offsets[0] : n * (uint64_t)key_len;
-        if (kb + (offsets ? (n + 1) * 8 : 0) + nw * 8 <= kSmallHostBuild)
-            return host_build_small(c, data, offsets, key_len, n, num_bits, k, words_in, words_out);
+        if (kb + (offsets ? (n + 1) * 8 : 0) + nw * 8 <= kSmallHostBuild) {
+            const int rc = host_build_small(c, data, offsets, key_len, n, num_bits, k, words_in, words_out);
+            if (!rc && crc) *crc = crc32_host(words_out, nw * 8, *crc);
+            return rc;
+        }
     }
     HIP_TRY(c->words.ensure(nw * 8));
     uint32_t* dw = (uint32_t*)c->words.p;
@@ -353,6 +358,9 @@ int host_build(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, uint32
         HIP_TRY(hipMemsetAsync(dw, 0, nw * 8, c->st));
     if (int rc = host_build_dev(c, data, offsets, key_len, n, num_bits, k, dw)) return rc;
     HIP_TRY(hipMemcpyAsync(words_out, dw, nw * 8, hipMemcpyDeviceToHost, c->st));
+    if (crc) {
+        if (int rc = crc32_dev(c, (const uint8_t*)dw, nw * 8, *crc, c->st, crc)) return rc;
+    }
     HIP_TRY(hipStreamSynchronize(c->st));
     return check_device_error(c);
 }
@@ -672,8 +680,8 @@ int lsmb_build_var(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, ui
     return host_build(c, data, offsets, 0, n, num_bits, k, words, (uint8_t*)words);
 }
 
-int lsmb_build_block(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
-                     uint32_t num_bits, uint32_t k, uint8_t* block, uint64_t block_len) {
+static int build_block(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
+                       uint32_t num_bits, uint32_t k, uint8_t* block, uint64_t block_len, uint32_t* crc) {
     if (int rc = check_filter(num_bits, k)) return rc;
     const uint64_t nw = nwords64(num_bits);
     const uint64_t size = 12 + 8 * nw;
@@ -691,6 +699,7 @@ int lsmb_build_block(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, 
         for (int b = 0; b < 4; b++) block[4 * i + b] = (uint8_t)(hdr[i] >> (8 * b));
     if (n == 0 || k == 0) {  // new() + no inserts: all-zero words
         memset(block + 12, 0, nw * 8);
+        if (crc) *crc = crc32_host(block, size, 0);
         return LSMB_OK;
     }
     if (n <= host_max_keys()) {
@@ -699,12 +708,27 @@ int lsmb_build_block(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, 
         std::vector<uint64_t> w(nw, 0);
         host_insert_batch(data, offsets, key_len, (!offsets && key_len == 0) ? 1 : n, num_bits, k, w.data());
         memcpy(block + 12, w.data(), nw * 8);
+        if (crc) *crc = crc32_host(block, size, 0);
         return LSMB_OK;
     }
     if (int rc = need_ctx(c, n)) return rc;
     DevGuard g(c->dev);
-    return host_build(c, data, offsets, key_len, n, num_bits, k, nullptr, block + 12);
+    if (crc) *crc = crc32_host(block, 12, 0);  // the header; the words' CRC is appended on the device
+    return host_build(c, data, offsets, key_len, n, num_bits, k, nullptr, block + 12, crc);
 }
+
+int lsmb_build_block(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
+                     uint32_t num_bits, uint32_t k, uint8_t* block, uint64_t block_len) {
+    return build_block(c, data, offsets, key_len, n, num_bits, k, block, block_len, nullptr);
+}
+
+int lsmb_build_block_crc(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
+                         uint32_t num_bits, uint32_t k, uint8_t* block, uint64_t block_len, uint32_t* crc) {
+    if (!crc) return fail(LSMB_EINVAL, "null crc");
+    return build_block(c, data, offsets, key_len, n, num_bits, k, block, block_len, crc);
+}
+
+
 
 uint64_t lsmb_host_max_keys(void) { return host_max_keys(); }
 
@@ -1061,8 +1085,11 @@ int fset_refresh(lsmb_fset* fs) {
     return LSMB_OK;
 }
 
+// expect_crc (optional): CRC-32 of the whole serialized block (`hdr` = its
+// 12-B header), checked against the device copy before the slot goes live.
 int fset_add_common(lsmb_fset* fs, const uint8_t* words_le, uint32_t num_bits, uint32_t k, const uint8_t* min_key,
-                    uint64_t min_len, const uint8_t* max_key, uint64_t max_len) {
+                    uint64_t min_len, const uint8_t* max_key, uint64_t max_len, const uint8_t* hdr = nullptr,
+                    const uint32_t* expect_crc = nullptr) {
     if (int rc = check_filter(num_bits, k)) return rc;
     if ((min_len && !min_key) || (max_len && !max_key)) return fail(LSMB_EINVAL, "null key range");
     if (min_len > UINT32_MAX || max_len > UINT32_MAX) return fail(LSMB_EINVAL, "range key too long");
@@ -1077,6 +1104,13 @@ int fset_add_common(lsmb_fset* fs, const uint8_t* words_le, uint32_t num_bits, u
     if (nw) {
         HIP_TRY(hipMemcpyAsync(S.words.p, words_le, nw * 8, hipMemcpyHostToDevice, fs->ust));
         HIP_TRY(hipStreamSynchronize(fs->ust));
+    }
+    if (expect_crc) {  // the copy now in HBM, not the host bytes, is what probes will read
+        uint32_t got = 0;
+        if (int rc = crc32_dev(fs->c, (const uint8_t*)S.words.p, nw * 8, crc32_host(hdr, 12, 0), fs->ust, &got))
+            return rc;
+        if (got != *expect_crc)
+            return fail(LSMB_ECORRUPT, "bloom block CRC-32 mismatch: expected %08x, device copy %08x", *expect_crc, got);
     }
     S.num_bits = num_bits;
     S.k = k;
@@ -1125,6 +1159,14 @@ int lsmb_fset_add(lsmb_fset* fs, const uint8_t* block, uint64_t len, const uint8
     uint32_t k, nb, nw;
     if (int rc = lsmb_deserialize_header(block, len, &k, &nb, &nw)) return rc;
     return fset_add_common(fs, block + 12, nb, k, min_key, min_len, max_key, max_len);
+}
+
+int lsmb_fset_add_crc(lsmb_fset* fs, const uint8_t* block, uint64_t len, uint32_t crc, const uint8_t* min_key,
+                      uint64_t min_len, const uint8_t* max_key, uint64_t max_len) {
+    if (!fs) return fail(LSMB_EINVAL, "null filter set");
+    uint32_t k, nb, nw;
+    if (int rc = lsmb_deserialize_header(block, len, &k, &nb, &nw)) return rc;
+    return fset_add_common(fs, block + 12, nb, k, min_key, min_len, max_key, max_len, block, &crc);
 }
 
 int lsmb_fset_add_words(lsmb_fset* fs, const uint64_t* words, uint32_t num_bits, uint32_t num_hashes,

@@ -77,6 +77,7 @@ struct lsmb_ctx {
     hipStream_t st = nullptr;
     lsmb::BuildTimers tm;
     lsmb::DevBuf ws_regions, ws_counts;  // partition / tiled workspace
+    lsmb::DevBuf crc_parts;              // CRC-32 workgroup partials (crc32.hip)
     lsmb::DevBuf ws_hashes;              // k_hash records (var-len / odd-length keys)
     lsmb::DevBuf err;                    // device error flag of the partition kernels
     uint32_t* err_host = nullptr;        // pinned mirror read at sync
@@ -127,5 +128,10 @@ void host_insert_batch(const uint8_t* data, const uint64_t* offsets, uint32_t ke
 // Reads (and clears) the kernels' device error flag.  Requires the work that
 // could set it to have completed.
 int check_device_error(lsmb_ctx* c);
+// CRC-32 (crc32fast::hash / zlib crc32) of device bytes appended to `crc`
+// (crc32.hip); synchronises `st`.
+int crc32_dev(lsmb_ctx* c, const uint8_t* d, uint64_t len, uint32_t crc, hipStream_t st, uint32_t* out);
+uint32_t crc32_host(const uint8_t* p, uint64_t len, uint32_t crc);
+uint32_t crc32_combine_host(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
 
 }  // namespace lsmb

@@ -57,6 +57,13 @@ SIGNATURES = {
     "lsmb_build_var": (ctypes.c_int, [vp, u8p, u64p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, u64p]),
     "lsmb_build_block": (ctypes.c_int, [vp, u8p, u64p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
                                         ctypes.c_uint32, u8p, ctypes.c_uint64]),
+    "lsmb_build_block_crc": (ctypes.c_int, [vp, u8p, u64p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
+                                            ctypes.c_uint32, u8p, ctypes.c_uint64, u32p]),
+    "lsmb_crc32": (ctypes.c_uint32, [ctypes.c_uint32, u8p, ctypes.c_uint64]),
+    "lsmb_crc32_combine": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]),
+    "lsmb_crc32_dev": (ctypes.c_int, [vp, ctypes.c_uint32, vp, ctypes.c_uint64, u32p, vp]),
+    "lsmb_fset_add_crc": (ctypes.c_int, [vp, u8p, ctypes.c_uint64, ctypes.c_uint32, u8p, ctypes.c_uint64, u8p,
+                                         ctypes.c_uint64]),
     "lsmb_probe": (ctypes.c_int, [vp, ctypes.POINTER(u64p), u32p, u32p, ctypes.c_uint32, u8p, u64p,
                                   ctypes.c_uint32, ctypes.c_uint64, u8p]),
     "lsmb_build_fixed_dev": (ctypes.c_int, [vp, vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
@@ -253,6 +260,30 @@ class Context:
         _check(lib().lsmb_build_block(self.h, _p(data, u8p), op, key_len, n, num_bits, k, _p(out, u8p), out.size))
         return out
 
+    def build_block_crc(self, data, num_bits, k, offsets=None, key_len=0, out=None):
+        """build_block + the block's CRC-32 (lsmb_build_block_crc) -> (block, crc)."""
+        data = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+        if offsets is not None:
+            offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+            n, op = offsets.size - 1, _p(offsets, u64p)
+        else:
+            n, op = (data.size // key_len if key_len else 0), None
+        if out is None:
+            out = np.empty(serialized_size(num_bits), dtype=np.uint8)
+        if data.size == 0:
+            data = np.zeros(1, np.uint8)
+        crc = ctypes.c_uint32()
+        _check(lib().lsmb_build_block_crc(self.h, _p(data, u8p), op, key_len, n, num_bits, k, _p(out, u8p),
+                                          out.size, ctypes.byref(crc)))
+        return out, crc.value
+
+    def crc32_dev(self, t, nbytes=None, crc=0, stream=None):
+        """CRC-32 of a device tensor's bytes (lsmb_crc32_dev), appended to crc."""
+        n = t.numel() * t.element_size() if nbytes is None else nbytes
+        out = ctypes.c_uint32()
+        _check(lib().lsmb_crc32_dev(self.h, crc, vp(t.data_ptr()), n, ctypes.byref(out), self._stream(stream)))
+        return out.value
+
     def probe(self, filters, data, offsets=None, key_len=0):
         """filters: [(words uint64 array, num_bits, k)] -> uint8 [n, ceil(F/8)] mask."""
         F = len(filters)
@@ -427,6 +458,13 @@ class FilterSet:
         hi, nhi = _key(max_key)
         return _check(lib().lsmb_fset_add(self.h, _p(b, u8p), n, _p(lo, u8p), nlo, _p(hi, u8p), nhi))
 
+    def add_checked(self, block, crc, min_key, max_key):
+        """add() that checks the block's CRC-32 on the device copy (lsmb_fset_add_crc)."""
+        b, n = _key(block)
+        lo, nlo = _key(min_key)
+        hi, nhi = _key(max_key)
+        return _check(lib().lsmb_fset_add_crc(self.h, _p(b, u8p), n, crc, _p(lo, u8p), nlo, _p(hi, u8p), nhi))
+
     def add_filter(self, filt, min_key, max_key):
         """filt: BloomFilter -> slot."""
         w = np.ascontiguousarray(filt.bits, dtype=np.uint64)
@@ -476,6 +514,16 @@ class FilterSet:
 def build_strategy(num_bits, n, k=7):
     """Device build strategy for (num_bits, k, n): lds / tiled / partition / atomic."""
     return lib().lsmb_build_strategy(num_bits, k, n).decode()
+
+
+def crc32(data, crc=0):
+    """CRC-32 of host bytes (lsmb_crc32; == zlib.crc32 == crc32fast::hash)."""
+    a, n = _key(data)
+    return int(lib().lsmb_crc32(crc, _p(a, u8p), n))
+
+
+def crc32_combine(crc_a, crc_b, len_b):
+    return int(lib().lsmb_crc32_combine(crc_a, crc_b, len_b))
 
 
 def build_sweeps(num_bits, n, k=7):
