@@ -518,6 +518,16 @@ def bench_e2e(ctx, keys, n, nb, k, reps=3):
                      "pcie_GBs": round((n * 16 + size) / t / 1e9, 1)}
     res["value"] = res["pageable"]["value"]
     res["unit"] = "Mkeys/s"
+    # the same flush with the block's CRC-32 computed on the device words
+    # (lsmb_build_block_crc), pinned keys
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        _, crc = ctx.build_block_crc(src, nb, k, key_len=16, out=block)
+        ts.append(time.perf_counter() - t0)
+    import zlib
+    res["with_crc32"] = {"ms": round(float(np.median(ts)) * 1e3, 2),
+                         "crc_equals_zlib": zlib.crc32(block) == crc}
     # SST-sized flushes: one lsmb_build_block call per table, sized like
     # SSTableBuilder::with_estimated_keys (builder.rs:74); latency per call
     # (H2D, kernels, D2H, sync) next to the 1-thread CPU oracle on the same
