@@ -16,6 +16,6 @@ wait
 for nv in "$@"; do
   name=${nv%%=*}
   /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o lib/liblsmbloom_$name.so \
-    build/bloom_build.o build/var_$name/bloom_probe.o build/capi.o build/multi.o build/stream.o
+    build/var_$name/bloom_probe.o $(ls build/*.o | grep -v '/bloom_probe.o$')
 done
 echo built: "$@"

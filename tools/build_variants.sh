@@ -16,6 +16,6 @@ wait
 for nv in "$@"; do
   name=${nv%%=*}
   /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o lib/liblsmbloom_$name.so \
-    build/var_$name/bloom_build.o build/bloom_probe.o build/capi.o build/multi.o build/stream.o
+    build/var_$name/bloom_build.o $(ls build/*.o | grep -v '/bloom_build.o$')
 done
 echo built: "$@"
