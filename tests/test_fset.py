@@ -310,6 +310,11 @@ def test_fset_mixed_size_classes(oracle, sizes):
         s = fs.add_filter(BloomFilter(w, k, nb), lo, hi)
         tables[s] = (w, nb, k, lo, hi)
         q.append(keys[:300])
+    # a k = 0 filter (may_contain vacuously true: only the range decides) is walked
+    nb0 = lsmbloom.params(1000, 0.01)[0]
+    w0 = np.zeros(lsmbloom.num_words(nb0), np.uint64)
+    s0 = fs.add_filter(BloomFilter(w0, 0, nb0), b"\x00", b"\x80")
+    tables[s0] = (w0, nb0, 0, b"\x00", b"\x80")
     fs.remove(2)
     del tables[2]
     q = np.concatenate(q + [keygen.key16(0x5EED0800, 0, 5000)])
