@@ -391,9 +391,10 @@ __global__ __launch_bounds__(kClassBlock) void k_fset_classes(Src src, uint64_t 
     extern __shared__ __align__(16) uint8_t smem_raw[];
     __shared__ RangedFilter fl[64];
     __shared__ FsetLds L;
-    __shared__ FsetClass C[kFsetMaxClasses];
+    __shared__ uint8_t mem[kFsetMaxClasses][64];  // member j -> descriptor (per-lane indexed)
+    const FsetClass* C = cl.cls;                  // uniform: scalar loads of the kernel arguments
     for (uint32_t f = threadIdx.x; f < nfilt; f += blockDim.x) fl[f] = filters[f];
-    for (uint32_t c = threadIdx.x; c < cl.ncls; c += blockDim.x) C[c] = cl.cls[c];
+    for (uint32_t i = threadIdx.x; i < cl.ncls * 64; i += blockDim.x) mem[i / 64][i % 64] = cl.cls[i / 64].mem[i % 64];
     stage_ranges(rg, L);
     __syncthreads();
     // class tables: thread w builds the 32 entries of word w, 32 members a pass
@@ -406,7 +407,7 @@ __global__ __launch_bounds__(kClassBlock) void k_fset_classes(Src src, uint64_t 
 #pragma unroll
                 for (int b = 0; b < 32; b++) acc[b] = 0;
                 for (uint32_t j = j0; j < nm && j < j0 + 32; j++) {
-                    const uint32_t x = fl[C[c].mem[j]].f.words32[w];
+                    const uint32_t x = fl[mem[c][j]].f.words32[w];
 #pragma unroll
                     for (int b = 0; b < 32; b++) acc[b] |= ((x >> b) & 1u) << (j - j0);
                 }
@@ -463,7 +464,7 @@ __global__ __launch_bounds__(kClassBlock) void k_fset_classes(Src src, uint64_t 
             while (acc) {
                 const uint32_t j = (uint32_t)__builtin_ctzll(acc);
                 acc &= acc - 1;
-                o |= 1ull << C[c].mem[j];
+                o |= 1ull << mem[c][j];
             }
         }
         uint64_t wm = rm & cl.walk_mask;

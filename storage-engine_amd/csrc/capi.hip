@@ -904,7 +904,6 @@ struct lsmb_fset {
     DevBuf ranges;  // the distinct boundary keys' bytes
     DevBuf points;  // FsetPoint[npts] then regmask[2 * npts + 1]
     DevBuf desc;    // RangedFilter[ndesc]
-    DevBuf classes; // FsetClass[cl.ncls]
     FsetRanges rg{};
     FsetClasses cl{};
     uint32_t ndesc = 0;
@@ -1070,12 +1069,8 @@ int fset_refresh(lsmb_fset* fs) {
         fs->cl.table_bytes = (uint32_t)off;
         fs->cl.walk_mask = all_desc & ~in_lds;
     }
-    HIP_TRY(fs->classes.ensure(sizeof(FsetClass) * kFsetMaxClasses));
-    if (!cls.empty())
-        HIP_TRY(hipMemcpyAsync(fs->classes.p, cls.data(), sizeof(FsetClass) * cls.size(), hipMemcpyHostToDevice,
-                               fs->ust));
-    fs->cl.cls = (const FsetClass*)fs->classes.p;
-    HIP_TRY(hipStreamSynchronize(fs->ust));  // blob, pbuf, d and cls are host temporaries
+    for (size_t i = 0; i < cls.size(); i++) fs->cl.cls[i] = cls[i];
+    HIP_TRY(hipStreamSynchronize(fs->ust));  // blob, pbuf and d are host temporaries
     fs->ndesc = (uint32_t)d.size();
     fs->shared_nb = d.empty() ? 0 : d[0].f.num_bits;
     fs->shared_k = d.empty() ? 0 : d[0].f.k;
@@ -1148,7 +1143,6 @@ void lsmb_fset_close(lsmb_fset* fs) {
         fs->ranges.release();
         fs->points.release();
         fs->desc.release();
-        fs->classes.release();
     }
     delete fs;
 }

@@ -153,7 +153,7 @@ struct FsetClass {
     uint8_t mem[64];   // member j -> descriptor index
 };
 struct FsetClasses {
-    const FsetClass* cls;  // ncls, device memory
+    FsetClass cls[kFsetMaxClasses];  // by value: the kernel reads them as uniform kernel arguments
     uint32_t ncls;
     uint32_t table_bytes;  // LDS bytes of all class tables
     uint64_t walk_mask;    // descriptors walked from L2
