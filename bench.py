@@ -422,6 +422,8 @@ def main():
         out["probe"] = bench_probe(ctx, dev, args, world, rank, max_over_ranks)
     if world == 1 and not args.no_exact10:
         out["c2_exact_10_bits_per_key"] = bench_exact10(ctx, keys, npg)
+    if world == 1:
+        out["c1_gpu"] = bench_c1_gpu(ctx, dev)
     if not args.no_e2e and rank == 0 and world == 1:
         out["e2e"] = bench_e2e(ctx, keys, npg, nb, k)
 
@@ -445,6 +447,61 @@ def main():
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_c1_gpu(ctx, dev, reps=20):
+    """C1's workload (configs[0]: build new(100000, 0.01) from 100 k key16
+    members, probe 100 k members + 100 k non-members) on the GPU, device-
+    resident keys, next to cpu_baseline.c1; the filter and the non-member
+    answers against the committed C1 fixture (tests/golden/c1_fixture.json)."""
+    import hashlib
+    import json
+
+    import numpy as np
+    import torch
+
+    import lsmbloom
+    n = 100_000
+    nb, k = lsmbloom.params(n, 0.01)
+    mem = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+    non = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+    ctx.gen_key16_dev(SEED_MEMBERS, 0, n, mem)
+    ctx.gen_key16_dev(SEED_FRESH, 0, n, non)
+    w = torch.zeros(lsmbloom.num_words(nb), dtype=torch.int64, device=dev)
+    q = torch.cat([mem, non])
+    out = torch.zeros((2 * n, 1), dtype=torch.uint8, device=dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    for _ in range(3):
+        w.zero_()
+        ctx.build_fixed_dev(mem, 16, n, nb, k, w)
+        ctx.probe_dev([(w, nb, k)], q, 2 * n, out, key_len=16)
+    torch.cuda.synchronize(dev)
+    ev[0].record()
+    for _ in range(reps):
+        w.zero_()
+        ctx.build_fixed_dev(mem, 16, n, nb, k, w)
+    ev[1].record()
+    ev[2].record()
+    for _ in range(reps):
+        ctx.probe_dev([(w, nb, k)], q, 2 * n, out, key_len=16)
+    ev[3].record()
+    torch.cuda.synchronize(dev)
+    b_ms, p_ms = ev[0].elapsed_time(ev[1]) / reps, ev[2].elapsed_time(ev[3]) / reps
+    res = {"workload": "C1 (configs[0]) on the GPU: build new(%d, 0.01) (%d bits, k=%d) from %d key16 members "
+                       "(zero + build), probe %d members + %d non-members" % (n, nb, k, n, n, n),
+           "build": {"ms": round(b_ms, 4), "value": round(n / (b_ms * 1e-3) / 1e6, 1), "unit": "Mkeys/s",
+                     "strategy": lsmbloom.build_strategy(nb, n, k)},
+           "probe": {"ms": round(p_ms, 4), "value": round(2 * n / (p_ms * 1e-3) / 1e6, 1), "unit": "Mkeys/s"}}
+    p = os.path.join(ROOT, "tests", "golden", "c1_fixture.json")
+    if os.path.exists(p):
+        fx = json.load(open(p))
+        hw = w.cpu().numpy().view(np.uint64)
+        blk = np.concatenate([np.array([k, nb, hw.size], dtype="<u4").view(np.uint8), hw.astype("<u8").view(np.uint8)])
+        m = out[n:].cpu().numpy().reshape(-1)
+        res["filter_equals_fixture"] = hashlib.sha256(blk.tobytes()).hexdigest() == fx["serialized_sha256"]
+        res["nonmember_answers_equal_fixture"] = hashlib.sha256(m.tobytes()).hexdigest() == fx["nonmember_probe_sha256"]
+        res["members_all_hit"] = bool(out[:n].bool().all().item())
+    return res
 
 
 def bench_exact10(ctx, keys, n, reps=10):
