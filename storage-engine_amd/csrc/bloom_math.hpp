@@ -58,24 +58,72 @@ struct Mod32 {
     }
 };
 
+// The same reduction for small moduli, d < 2^14 (SST-sized filters: the
+// store's new(1000, 0.01) is 9 568 bits).  x's four 16-bit limbs times
+// t_j = 2^(16 j) mod d sum to y < 2^16 + 3·2^16·d < 2^32, so y/d < 2^18 + 1;
+// one f32 estimate q = trunc(f32(y)·f32(1/d)) is then within 1 of floor(y/d)
+// (f32(y) is off by < y·2^-24, i.e. < 0.02 after the division, and the two
+// other roundings by < 2^18·2^-23), and one fix-up each way finishes it.
+// Full-rate 24-bit multiplies and f32 only: no 64-bit products, no f64.
+struct Mod14 {
+    uint32_t d, t16, t32, t48;  // 2^(16 j) mod d
+    uint32_t t64, dt;           // 2^64 mod d, d - t64 (the walk's carry step)
+    float inv;                  // 1.0f / d
+
+    static Mod14 make(uint32_t d32) {
+        Mod14 r;
+        r.d = d32;
+        r.t16 = (uint32_t)((1ull << 16) % d32);
+        r.t32 = (uint32_t)((1ull << 32) % d32);
+        r.t48 = (uint32_t)((1ull << 48) % d32);
+        r.t64 = (uint32_t)((uint64_t)(((unsigned __int128)1 << 64) % d32));
+        r.dt = d32 - r.t64;
+        r.inv = 1.0f / (float)d32;
+        return r;
+    }
+    static LSMB_HD bool fits(uint32_t d) { return d >= 1 && d < (1u << 14); }
+
+    // a·b for a, b < 2^24 (exact when the product fits 32 bits): one
+    // full-rate v_mul_u32_u24 on the device instead of a quarter-rate mul_lo
+    static LSMB_HD uint32_t mul24(uint32_t a, uint32_t b) {
+#ifdef __HIP_DEVICE_COMPILE__
+        return __umul24(a, b);
+#else
+        return a * b;
+#endif
+    }
+    LSMB_HD uint32_t reduce(uint64_t x) const {
+        const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+        const uint32_t y = (lo & 0xFFFFu) + mul24(lo >> 16, t16) + mul24(hi & 0xFFFFu, t32) + mul24(hi >> 16, t48);
+        const uint32_t q = (uint32_t)((float)y * inv);
+        uint32_t r = y - mul24(q, d);  // in [-d, 2d), wrapped (q < 2^19, d < 2^14)
+        const uint32_t a = r + d;
+        r = a < r ? a : r;       // q one too high: r wrapped below 0
+        const uint32_t b = r - d;
+        return b < r ? b : r;    // q one too low: r in [d, 2d)
+    }
+};
+
 // k positions of one key, i = 0, 1, ..., for d <= 2^31 (all sums fit 32 bits).
 // Position i+1 = (pos_i + h2 - c*2^64) mod d, where c = 1 when the wrapping
 // u64 sum h1 + i*h2 (src/bloom/mod.rs:194) carries out; so the two possible
 // increments, h2 mod d and (h2 - 2^64) mod d, are reduced once per key and
 // each step is a 64-bit add with carry, a select, an add and one conditional
 // subtract.
-struct Walk32 {
+template <class M>
+struct Walk32T {
+    using Mod = M;
     uint64_t x, h2;
     uint32_t r, s0, s1, d;
 
-    LSMB_HD Walk32(const Mod32& md, uint64_t h1, uint64_t h2_) : x(h1), h2(h2_), d(md.d) {
+    LSMB_HD Walk32T(const M& md, uint64_t h1, uint64_t h2_) : x(h1), h2(h2_), d(md.d) {
         r = md.reduce(h1);
         s0 = md.reduce(h2_);
         const uint32_t t = s0 + md.dt;  // < 2d <= 2^32
         s1 = t - md.d < t ? t - md.d : t;
     }
     LSMB_HD uint32_t pos() const { return r; }
-    LSMB_HD void next(const Mod32&) {
+    LSMB_HD void next(const M&) {
         uint64_t nx;
         const bool carry = __builtin_add_overflow(x, h2, &nx);
         x = nx;
@@ -84,8 +132,12 @@ struct Walk32 {
     }
 };
 
+using Walk32 = Walk32T<Mod32>;
+using Walk14 = Walk32T<Mod14>;  // d < 2^14 (Mod14's reduction)
+
 // The same walk for any d < 2^32 (64-bit intermediate sums).
 struct Walk64 {
+    using Mod = Mod32;
     uint64_t x, h2;
     uint32_t r, s;
 

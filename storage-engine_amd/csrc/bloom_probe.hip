@@ -54,7 +54,7 @@ __device__ __forceinline__ void store_row(uint8_t* out, uint64_t i, uint32_t str
 // (16-B keys, 8-bit entries, k = 7) instantiations run 1024-thread
 // workgroups, two per CU, so a CU builds it twice instead of eight times.
 template <class Src, typename T, class W, int K, int BS = 256>
-__global__ __launch_bounds__(BS) void k_probe_sliced(Src src, uint64_t n, Mod32 md, uint32_t k_,
+__global__ __launch_bounds__(BS) void k_probe_sliced(Src src, uint64_t n, typename W::Mod md, uint32_t k_,
                                                       uint32_t num_bits,
                                                       const ProbeFilter* __restrict__ filters,
                                                       uint32_t nfilt, uint32_t stride,
@@ -315,10 +315,11 @@ __global__ __launch_bounds__(256) void k_fset_probe(Src src, uint64_t n, const R
 // descriptor.  A key pays one region lookup for the range checks, then k LDS
 // reads ANDed over all in-range filters at once (bits read from L2 per
 // filter in k_fset_probe).
-template <class Src, typename T, int K, int BS = 256>
+// W: Walk14 (the set's num_bits < 2^14, e.g. SST filters) or Walk32.
+template <class Src, typename T, int K, int BS = 256, class W = Walk32>
 __global__ __launch_bounds__(BS) void k_fset_sliced(Src src, uint64_t n, const RangedFilter* __restrict__ filters,
                                                      uint32_t nfilt, FsetRanges rg, uint32_t k_,
-                                                     uint64_t* __restrict__ out) {
+                                                     typename W::Mod md, uint64_t* __restrict__ out) {
     extern __shared__ __align__(16) uint8_t smem_raw[];
     __shared__ RangedFilter fl[64];
     __shared__ FsetLds L;
@@ -327,7 +328,6 @@ __global__ __launch_bounds__(BS) void k_fset_sliced(Src src, uint64_t n, const R
     stage_ranges(rg, L);
     __syncthreads();
     const uint32_t num_bits = fl[0].f.num_bits;
-    const Mod32 md = fl[0].f.md;
     bool ident = true;  // slots 0..nfilt-1 all live: table bit f is output bit f
     for (uint32_t f = 0; f < nfilt; f++) ident = ident && fl[f].f.out_bit == f;
     const uint32_t nw32 = (num_bits + 31) / 32;  // num_bits <= 2^19 here: no wrap
@@ -352,7 +352,7 @@ __global__ __launch_bounds__(BS) void k_fset_sliced(Src src, uint64_t n, const R
         const uint64_t kl = src.key_len(i);
         T m = (T)L.regmask[key_region(prefix16(kp, kl), kp, kl, L, npts)];
         if (m) {
-            Walk32 pw(md, h.lo, h.hi);
+            W pw(md, h.lo, h.hi);
             if (K > 0) {
 #pragma unroll
                 for (int j = 0; j < K; j++) {
@@ -532,19 +532,23 @@ hipError_t fset_probe_with(const Src& src, uint64_t n, const RangedFilter* df, u
         const size_t tsz = nfilt <= 8 ? 1 : nfilt <= 16 ? 2 : nfilt <= 32 ? 4 : 8;
         const size_t smem = (size_t)(((uint64_t)shared_nb + 31) / 32) * 32 * tsz;
         if (smem <= 64 * 1024) {
-            auto go = [&](auto kern, uint32_t bs = 256) {
+            const Mod32 m32 = Mod32::make(shared_nb);
+            auto go = [&](auto kern, auto md, uint32_t bs = 256) {
                 hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
                 const uint64_t gb = bs == 256 ? g : std::min<uint64_t>((n + bs - 1) / bs, probe_wgs_per_cu(2) * num_cus);
                 kern<<<dim3((uint32_t)std::max<uint64_t>(gb, 1)), dim3(bs), smem, st>>>(src, n, df, nfilt, rg,
-                                                                                           shared_k, out);
+                                                                                           shared_k, md, out);
             };
             if (tsz == 1) {
-                if (shared_k == 7 && std::is_same<Src, Fixed16>::value) go(k_fset_sliced<Src, uint8_t, 7, 1024>, 1024);
-                else if (shared_k == 7) go(k_fset_sliced<Src, uint8_t, 7>);
-                else go(k_fset_sliced<Src, uint8_t, 0>);
-            } else if (tsz == 2) go(k_fset_sliced<Src, uint16_t, 0>);
-            else if (tsz == 4) go(k_fset_sliced<Src, uint32_t, 0>);
-            else go(k_fset_sliced<Src, uint64_t, 0>);
+                if (shared_k == 7 && std::is_same<Src, Fixed16>::value && Mod14::fits(shared_nb))
+                    go(k_fset_sliced<Src, uint8_t, 7, 1024, Walk14>, Mod14::make(shared_nb), 1024);
+                else if (shared_k == 7 && std::is_same<Src, Fixed16>::value)
+                    go(k_fset_sliced<Src, uint8_t, 7, 1024>, m32, 1024);
+                else if (shared_k == 7) go(k_fset_sliced<Src, uint8_t, 7>, m32);
+                else go(k_fset_sliced<Src, uint8_t, 0>, m32);
+            } else if (tsz == 2) go(k_fset_sliced<Src, uint16_t, 0>, m32);
+            else if (tsz == 4) go(k_fset_sliced<Src, uint32_t, 0>, m32);
+            else go(k_fset_sliced<Src, uint64_t, 0>, m32);
             return hipGetLastError();
         }
     }
@@ -569,24 +573,28 @@ hipError_t probe_with(const Src& src, uint64_t n, const ProbeFilter* hf, uint32_
         const size_t tsz = nfilt <= 8 ? 1 : nfilt <= 16 ? 2 : 4;
         const size_t smem = ent * tsz;
         if (smem <= 64 * 1024) {
-            auto go = [&](auto kern, uint32_t bs = 256) {
+            auto go = [&](auto kern, auto md, uint32_t bs = 256) {
                 hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
                 const uint64_t gb = bs == 256 ? g : std::min<uint64_t>((n + bs - 1) / bs, probe_wgs_per_cu(1) * num_cus);
-                kern<<<dim3((uint32_t)std::max<uint64_t>(gb, 1)), dim3(bs), smem, st>>>(src, n, hf[0].md, hf[0].k, nb,
+                kern<<<dim3((uint32_t)std::max<uint64_t>(gb, 1)), dim3(bs), smem, st>>>(src, n, md, hf[0].k, nb,
                                                                                            df, nfilt, stride, out);
             };
+            const Mod32 m32 = hf[0].md;
             const bool w32 = fits_walk32(nb), k7 = hf[0].k == 7;
             if (tsz == 1) {
-                if (w32 && k7 && std::is_same<Src, Fixed16>::value) go(k_probe_sliced<Src, uint8_t, Walk32, 7, 1024>, 1024);
-                else if (w32 && k7) go(k_probe_sliced<Src, uint8_t, Walk32, 7>);
-                else if (w32) go(k_probe_sliced<Src, uint8_t, Walk32, 0>);
-                else go(k_probe_sliced<Src, uint8_t, Walk64, 0>);
+                if (k7 && std::is_same<Src, Fixed16>::value && Mod14::fits(nb))
+                    go(k_probe_sliced<Src, uint8_t, Walk14, 7, 1024>, Mod14::make(nb), 1024);
+                else if (w32 && k7 && std::is_same<Src, Fixed16>::value)
+                    go(k_probe_sliced<Src, uint8_t, Walk32, 7, 1024>, m32, 1024);
+                else if (w32 && k7) go(k_probe_sliced<Src, uint8_t, Walk32, 7>, m32);
+                else if (w32) go(k_probe_sliced<Src, uint8_t, Walk32, 0>, m32);
+                else go(k_probe_sliced<Src, uint8_t, Walk64, 0>, m32);
             } else if (tsz == 2) {
-                if (w32) go(k_probe_sliced<Src, uint16_t, Walk32, 0>);
-                else go(k_probe_sliced<Src, uint16_t, Walk64, 0>);
+                if (w32) go(k_probe_sliced<Src, uint16_t, Walk32, 0>, m32);
+                else go(k_probe_sliced<Src, uint16_t, Walk64, 0>, m32);
             } else {
-                if (w32) go(k_probe_sliced<Src, uint32_t, Walk32, 0>);
-                else go(k_probe_sliced<Src, uint32_t, Walk64, 0>);
+                if (w32) go(k_probe_sliced<Src, uint32_t, Walk32, 0>, m32);
+                else go(k_probe_sliced<Src, uint32_t, Walk64, 0>, m32);
             }
             return hipGetLastError();
         }

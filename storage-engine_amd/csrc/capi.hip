@@ -191,7 +191,7 @@ int build_dev_ws(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_
 // Host single-key walks (the same arithmetic the kernels run).
 template <class W, class F>
 void walk_key(const uint8_t* key, uint64_t len, uint32_t num_bits, uint32_t k, F&& f) {
-    const Mod32 md = Mod32::make(num_bits);
+    const typename W::Mod md = W::Mod::make(num_bits);
     const H128 h = xxh3_128(key, len);
     W w(md, h.lo, h.hi);
     for (uint32_t i = 0; i < k; i++) {
@@ -202,7 +202,9 @@ void walk_key(const uint8_t* key, uint64_t len, uint32_t num_bits, uint32_t k, F
 
 template <class F>
 void for_positions(const uint8_t* key, uint64_t len, uint32_t num_bits, uint32_t k, F&& f) {
-    if (fits_walk32(num_bits))
+    if (Mod14::fits(num_bits))
+        walk_key<Walk14>(key, len, num_bits, k, f);
+    else if (fits_walk32(num_bits))
         walk_key<Walk32>(key, len, num_bits, k, f);
     else
         walk_key<Walk64>(key, len, num_bits, k, f);

@@ -71,6 +71,20 @@ def test_exact_mod_strength_reduction_vs_oracle(oracle):
             assert lsmbloom.positions(key, m, k) == oracle.positions(key, m, k), (m, key, k)
 
 
+def test_small_moduli_reduction_vs_oracle(oracle):
+    """Moduli below 2^14 take Mod14 (16-bit limbs, an f32 quotient estimate,
+    one fix-up each way): random and edge moduli, random keys and k, against
+    the oracle's literal 64-bit %."""
+    rng = np.random.default_rng(17)
+    mods = [1, 2, 3, 5, 7, 255, 256, 257, 1023, 1024, 4095, 4096, 9568, 9569, 16381, 16383]
+    mods += [int(x) for x in rng.integers(1, 2**14, size=300)]
+    for m in mods:
+        for t in range(20):
+            key = rng.bytes(int(rng.integers(0, 48)))
+            k = int(rng.integers(1, 33))
+            assert lsmbloom.positions(key, m, k) == oracle.positions(key, m, k), (m, key, k)
+
+
 def test_single_key_scenarios_match_golden():
     # BloomFilter::insert / may_contain on the host words (reference scenarios)
     for sc in KATS["scenarios"]:
