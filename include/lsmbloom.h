@@ -47,7 +47,7 @@ extern "C" {
 #define LSMB_ECORRUPT (-4) /* serialized filter fails validation               */
 #define LSMB_ENOMEM (-5)   /* device or pinned-host allocation failed          */
 
-#define LSMB_ABI_VERSION 4
+#define LSMB_ABI_VERSION 5 /* 5: sweep builds, block CRC-32 */
 
 typedef struct lsmb_ctx lsmb_ctx; /* one GPU: stream, events, scratch arenas */
 
