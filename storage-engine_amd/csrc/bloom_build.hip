@@ -27,9 +27,6 @@
 //              atomics on the filter (the memory-side atomic unit serves ~20 G
 //              scattered requests/s chip-wide; 7e8 of them would take ~35 ms).
 //   Atomic     few keys into a huge filter: direct global atomicOr.
-#include <climits>
-#include <cmath>
-#include <cstring>
 #include <mutex>
 #include <vector>
 
@@ -50,12 +47,6 @@
 #endif
 #ifndef LSMB_STORE_AUX
 #define LSMB_STORE_AUX 0  // pass A region stores' cache policy bits (measurement variants)
-#endif
-#ifndef LSMB_SABL
-#define LSMB_SABL 0  // k_sort ablations (tools only): 1 = no claims, 2 = no scatter, 4 = no tile stores
-#endif
-#ifndef LSMB_RABL
-#define LSMB_RABL 0  // k_apply_runs ablations (tools only): 1 = no LDS ORs, 2 = no entry loads
 #endif
 #ifndef LSMB_APPLY_U
 #define LSMB_APPLY_U 8  // pass B: 16-B region loads in flight per lane
@@ -608,8 +599,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
 // u + 8 (or u + w in a last group of w < 8 bins): the same XCD under
 // round-robin dispatch, close in time, so the second read of the bin's
 // regions mostly hits in L2 / MALL.
-// P: 16-B pieces per counted unit (4: k_bin's 64-B segments; 1: k_sortr's chunks).
-template <int SL = kSliceLog2, int P = 4>
+template <int SL = kSliceLog2>
 __global__ __launch_bounds__(kApplyBlock) void k_apply(const uint64_t* __restrict__ regions,
                                                        const uint32_t* __restrict__ counts,
                                                        uint32_t grid, uint32_t cap, uint32_t nbins,
@@ -654,8 +644,8 @@ __global__ __launch_bounds__(kApplyBlock) void k_apply(const uint64_t* __restric
         for (uint32_t j = 0; j < nreg; j++) {
             const uint32_t r = wave + j * NWAVE;
             const uint32_t nseg = __shfl(cnt, (int)j);
-            const uint4* src = reinterpret_cast<const uint4*>(regions + ((uint64_t)r * nbins + b) * cap * (2 * P));
-            const uint32_t n16 = nseg * P;  // 16-B pieces (2 words, 6 offsets)
+            const uint4* src = reinterpret_cast<const uint4*>(regions + ((uint64_t)r * nbins + b) * cap * kSegWords);
+            const uint32_t n16 = nseg * (kSegWords / 2);  // 16-B pieces (2 words, 6 offsets)
             constexpr uint32_t U = LSMB_APPLY_U;           // loads in flight per lane
             for (uint32_t i0 = 0; i0 < n16; i0 += 64 * U) {
                 uint4 v[U];
@@ -686,431 +676,6 @@ __global__ __launch_bounds__(kApplyBlock) void k_apply(const uint64_t* __restric
         for (uint32_t i = tid; i < nw2; i += kApplyBlock) g2[i] = f2[i];
         __syncthreads();
     }
-}
-
-// ---------------------------------------------------------------- Partition, sorted tiles
-// Pass A as a per-tile counting sort (k_sort) instead of per-slice rings
-// flushed every phase (k_bin).  A workgroup takes a tile of BLOCK * KPL keys:
-//   claim    each lane hashes and walks its KPL keys; every position claims a
-//            rank within its bin with one ds_add_rtn on the bin's counter (the
-//            return is only needed two barriers later, so it overlaps the
-//            next key's hash);
-//   barrier
-//   scan     thread i owns bin i: an exclusive scan of the counters gives each
-//            bin's start in the tile; the inclusive ends go to the tile's row
-//            of the run table (u16, coalesced) and the counters are zeroed;
-//   barrier (x2: the scan's wave totals)
-//   scatter  entry start[bin] + rank = in-bin offset (ds_write_b32);
-//   barrier
-//   write    the tile's entries, now grouped by bin, are packed 3 per u64
-//            (entry e in word e/3 at bits SL*(e%3)) and stored as one dense,
-//            fully coalesced 16-B-per-lane stream (no partial lines, no
-//            capacity per bin, so no overflow path: a tile of identical keys
-//            is one long run).  The next tile's claims follow without a
-//            barrier (they touch only the zeroed counters).
-// Four barriers per tile of KPL keys per lane (k_bin: two per key).
-// Pass B (k_apply_runs) gives each bin to one workgroup, which reads the bin's
-// run [end[t][b-1], end[t][b]) of every tile t.
-struct PassS {
-    uint32_t b0, nb;      // this sweep's bins [b0, b0 + nb)
-    uint64_t ntiles;      // tiles of this chunk (BLOCK * KPL keys each)
-    uint32_t tstride;     // u64 words per tile in `ents`
-    uint32_t rstride;     // u16 entries per tile row of `runs`
-    uint64_t* ents;       // [ntiles][tstride] packed in-bin offsets, grouped by bin
-    uint16_t* runs;       // [ntiles][rstride]: inclusive end of bin b0 + j's run, j < nb
-};
-
-constexpr uint32_t kSortMaxBins = 1024;  // bins per sweep (counters + starts: 8 KiB)
-constexpr uint32_t kSortLdsFixed = (2 * kSortMaxBins + 32) * 4;
-constexpr uint32_t kNoPos = 0xFFFFFFFFu;
-
-template <class Src, class W, int KMAX, bool EXACT, bool FULL, int SL, int BLOCK, int KPL>
-__global__ __launch_bounds__(BLOCK) void k_sort(Src src, uint64_t n, Mod32 md, uint32_t k_, PassS a) {
-    constexpr uint32_t kMask = (1u << SL) - 1;
-    constexpr int NP = KPL * KMAX;        // positions per lane per tile
-    constexpr uint32_t T = BLOCK * NP;    // tile capacity, entries
-    static_assert(T < 65536, "run ends are u16");
-    constexpr uint32_t BPT = (kSortMaxBins + BLOCK - 1) / BLOCK;  // bins per scan thread
-    extern __shared__ uint32_t sm[];
-    uint32_t* cnt = sm;                        // [kSortMaxBins]
-    uint32_t* start = sm + kSortMaxBins;       // [kSortMaxBins]
-    uint32_t* wsum = start + kSortMaxBins;     // [NWAVE], [16] = tile total
-    uint32_t* ent = wsum + 32;                 // [T]
-    const uint32_t k = EXACT ? (uint32_t)KMAX : k_;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nb = a.nb;
-    const uint32_t lim = nb << SL;
-    for (uint32_t i = tid; i < kSortMaxBins; i += BLOCK) cnt[i] = 0;
-    // entries past a tile's total are packed (never applied) with the rest of
-    // their word: keep them < 2^SL so they cannot spill into a neighbour field
-    for (uint32_t i = tid; i < T; i += BLOCK) ent[i] = 0;
-
-    using Pre = typename Src::Pre;
-    auto key_index = [&](uint64_t t, int j) { return t * (uint64_t)(BLOCK * KPL) + (uint64_t)j * BLOCK + tid; };
-    Pre pre[KPL];
-    uint64_t t = blockIdx.x;
-#pragma unroll
-    for (int j = 0; j < KPL; j++) pre[j] = src.fetch(key_index(t, j), t < a.ntiles && key_index(t, j) < n);
-    __syncthreads();
-
-    for (; t < a.ntiles; t += gridDim.x) {  // block-uniform
-        // 1. hash, walk, claim
-        uint32_t p[NP], r[NP];
-#pragma unroll
-        for (int j = 0; j < KPL; j++) {
-            const uint64_t i = key_index(t, j);
-            const bool ok = i < n;
-            const H128 h = src.hash_pre(pre[j], i);
-            W walk(md, h.lo, h.hi);
-#pragma unroll
-            for (int q = 0; q < KMAX; q++) {
-                const int e = j * KMAX + q;
-                p[e] = kNoPos;
-                r[e] = 0;
-                if (EXACT || (uint32_t)q < k) {
-                    const uint32_t lp = walk.pos() - (FULL ? 0u : (a.b0 << SL));
-                    if (ok && (FULL || lp < lim)) {
-                        p[e] = lp;
-                        r[e] = (LSMB_SABL & 1) ? (lp & 31) : atomicAdd(cnt + (lp >> SL), 1u);
-                    }
-                    if (q + 1 < KMAX) walk.next(md);
-                }
-            }
-        }
-        {
-            const uint64_t tn = t + gridDim.x;
-#pragma unroll
-            for (int j = 0; j < KPL; j++) pre[j] = src.fetch(key_index(tn, j), tn < a.ntiles && key_index(tn, j) < n);
-        }
-        lds_barrier();
-
-        // 2. scan: thread tid owns bins [tid*BPT, tid*BPT + BPT)
-        uint32_t c[BPT], sum = 0;
-#pragma unroll
-        for (uint32_t u = 0; u < BPT; u++) {
-            const uint32_t b = tid * BPT + u;
-            c[u] = b < nb ? cnt[b] : 0u;
-            sum += c[u];
-        }
-        uint32_t x = sum;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(x, d);
-            if (lane >= (uint32_t)d) x += y;
-        }
-        if (lane == 63) wsum[wave] = x;
-        lds_barrier();
-        uint32_t run = x - sum;
-        for (uint32_t v = 0; v < wave; v++) run += wsum[v];
-        uint16_t* rrow = a.runs + t * a.rstride;
-#pragma unroll
-        for (uint32_t u = 0; u < BPT; u++) {
-            const uint32_t b = tid * BPT + u;
-            if (b < nb) {
-                start[b] = run;
-                cnt[b] = 0;
-                run += c[u];
-                rrow[b] = (uint16_t)run;
-            }
-        }
-        if (tid == BLOCK - 1) wsum[16] = run;  // the tile's total
-        lds_barrier();
-
-        // 3. scatter
-#pragma unroll
-        for (int e = 0; e < NP; e++)
-            if (p[e] != kNoPos) {
-                if (LSMB_SABL & 2) wsum[20 + (e & 7)] = p[e] + r[e];
-                else ent[start[p[e] >> SL] + r[e]] = p[e] & kMask;
-            }
-        lds_barrier();
-
-        // 4. write the tile: 6 entries (two packed u64) per lane per store
-        const uint32_t nch = (wsum[16] + 5) / 6;
-        uint4* dst = reinterpret_cast<uint4*>(a.ents + t * a.tstride);
-        for (uint32_t ch = tid; ch < nch; ch += BLOCK) {
-            const uint2 e0 = *reinterpret_cast<const uint2*>(ent + 6 * ch);
-            const uint2 e1 = *reinterpret_cast<const uint2*>(ent + 6 * ch + 2);
-            const uint2 e2 = *reinterpret_cast<const uint2*>(ent + 6 * ch + 4);
-            const uint2 w0 = pack3w<SL>(e0.x, e0.y, e1.x), w1 = pack3w<SL>(e1.y, e2.x, e2.y);
-            if (LSMB_SABL & 4) wsum[28] = w0.x ^ w0.y ^ w1.x ^ w1.y;
-            else dst[ch] = make_uint4(w0.x, w0.y, w1.x, w1.y);
-        }
-    }
-}
-
-// Pass A, sorted tiles into regions (k_sortr; the default).  The same per-tile
-// counting sort as k_sort, but each bin's run is appended to the workgroup's
-// private region for that bin, so pass B (k_apply) streams long contiguous
-// regions instead of ~100-B runs scattered over every tile:
-//   scan     over the runs' 16-B chunk counts ceil(c_b / 6): bin b's entries
-//            start at entry 6 Q_b; the pad slots after its c_b entries get a
-//            sentinel, the chunk -> bin map gets b for its chunks, and the
-//            region's fill advances (a run that does not fit the region's
-//            capacity, adversarial duplicates only, is set with exact global
-//            atomics instead: pass B reads the words after pass A);
-//   write    lane q packs chunk q (sentinels -> the chunk's first entry, a
-//            bit set twice is a no-op) and stores it at its bin's region
-//            position: a run's chunks are consecutive, so one store
-//            instruction writes ~10 runs of ~90 contiguous bytes.
-struct PassR {
-    uint32_t b0, nb;      // this sweep's bins [b0, b0 + nb)
-    uint32_t nbins, cap;  // bins of the filter; region capacity, 16-B chunks
-    uint64_t ntiles;
-    uint64_t* regions;    // [grid][nbins][cap] chunks (two u64 each)
-    uint32_t* counts;     // [nbins][grid] chunks written
-    uint32_t* gw;         // filter words (region overflow only)
-};
-
-constexpr int32_t kRunOvf = INT32_MIN;
-
-// Entry slots: T positions plus up to 5 pad slots per bin (runs padded to
-// whole 6-entry chunks); chunk map: T / 6 + one partial chunk per bin.
-template <int KPL, int KMAX>
-constexpr uint32_t sortr_ent_slots() {
-    return 1024 * KPL * KMAX + 5 * kSortMaxBins + 8;
-}
-template <int KPL, int KMAX>
-constexpr uint32_t sortr_lds_bytes() {
-    return (4 * kSortMaxBins + 32) * 4 + sortr_ent_slots<KPL, KMAX>() * 4 +
-           ((1024 * KPL * KMAX) / 6 + kSortMaxBins + 2) * 2;
-}
-
-template <class Src, class W, int KMAX, bool EXACT, bool FULL, int SL, int KPL>
-__global__ __launch_bounds__(1024) void k_sortr(Src src, uint64_t n, Mod32 md, uint32_t k_, PassR a) {
-    constexpr int BLOCK = 1024;
-    constexpr uint32_t kMask = (1u << SL) - 1;
-    constexpr int NP = KPL * KMAX;
-    static_assert(sortr_lds_bytes<KPL, KMAX>() <= kLdsBytes, "LDS");
-    extern __shared__ uint32_t sm[];
-    uint32_t* cnt = sm;                          // [1024] claims per bin
-    uint32_t* qst = cnt + kSortMaxBins;          // [1024] first chunk of the bin's run in the tile
-    int32_t* dst = (int32_t*)(qst + kSortMaxBins);  // [1024] region chunk of tile chunk 0 (or kRunOvf)
-    uint32_t* fill = (uint32_t*)(dst + kSortMaxBins);  // [1024] region chunks written
-    uint32_t* wsum = fill + kSortMaxBins;        // [16] wave totals, [16] = tile chunks
-    uint32_t* ent = wsum + 32;                   // [T + 5 * 1024 + 8] (padded runs)
-    uint16_t* cmap = (uint16_t*)(ent + sortr_ent_slots<KPL, KMAX>());  // [T/6 + 1024 + 2] chunk -> bin
-    const uint32_t k = EXACT ? (uint32_t)KMAX : k_;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nb = a.nb;
-    const uint32_t lim = nb << SL;
-    cnt[tid] = 0;
-    fill[tid] = 0;
-    uint4* rgn = reinterpret_cast<uint4*>(a.regions + (uint64_t)blockIdx.x * a.nbins * a.cap * 2);
-
-    using Pre = typename Src::Pre;
-    auto key_index = [&](uint64_t t, int j) { return t * (uint64_t)(BLOCK * KPL) + (uint64_t)j * BLOCK + tid; };
-    Pre pre[KPL];
-    uint64_t t = blockIdx.x;
-#pragma unroll
-    for (int j = 0; j < KPL; j++) pre[j] = src.fetch(key_index(t, j), t < a.ntiles && key_index(t, j) < n);
-    __syncthreads();
-
-    for (; t < a.ntiles; t += gridDim.x) {  // block-uniform
-        // 1. hash, walk, claim
-        uint32_t p[NP], r[NP];
-#pragma unroll
-        for (int j = 0; j < KPL; j++) {
-            const uint64_t i = key_index(t, j);
-            const bool ok = i < n;
-            const H128 h = src.hash_pre(pre[j], i);
-            W walk(md, h.lo, h.hi);
-#pragma unroll
-            for (int q = 0; q < KMAX; q++) {
-                const int e = j * KMAX + q;
-                p[e] = kNoPos;
-                r[e] = 0;
-                if (EXACT || (uint32_t)q < k) {
-                    const uint32_t lp = walk.pos() - (FULL ? 0u : (a.b0 << SL));
-                    if (ok && (FULL || lp < lim)) {
-                        p[e] = lp;
-                        r[e] = atomicAdd(cnt + (lp >> SL), 1u);
-                    }
-                    if (q + 1 < KMAX) walk.next(md);
-                }
-            }
-        }
-        {
-            const uint64_t tn = t + gridDim.x;
-#pragma unroll
-            for (int j = 0; j < KPL; j++) pre[j] = src.fetch(key_index(tn, j), tn < a.ntiles && key_index(tn, j) < n);
-        }
-        lds_barrier();
-
-        // 2. scan over the runs' chunk counts (thread tid owns bin tid)
-        const uint32_t c = tid < nb ? cnt[tid] : 0u;
-        const uint32_t nch = (c + 5) / 6;
-        uint32_t x = nch;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(x, d);
-            if (lane >= (uint32_t)d) x += y;
-        }
-        if (lane == 63) wsum[wave] = x;
-        lds_barrier();
-        uint32_t q0 = x - nch;
-        for (uint32_t v = 0; v < wave; v++) q0 += wsum[v];
-        if (tid < nb) {
-            cnt[tid] = 0;
-            qst[tid] = q0;
-            for (uint32_t i = c; i < 6 * nch; i++) ent[6 * q0 + i] = kNoPos;
-            for (uint32_t i = 0; i < nch; i++) cmap[q0 + i] = (uint16_t)tid;
-            const uint32_t f = fill[tid];
-            if (f + nch <= a.cap) {
-                dst[tid] = (int32_t)((a.b0 + tid) * a.cap + f) - (int32_t)q0;
-                fill[tid] = f + nch;
-            } else {
-                dst[tid] = kRunOvf;
-            }
-        }
-        if (tid == BLOCK - 1) wsum[16] = q0 + nch;  // the tile's chunks
-        lds_barrier();
-
-        // 3. scatter
-#pragma unroll
-        for (int e = 0; e < NP; e++)
-            if (p[e] != kNoPos) ent[6 * qst[p[e] >> SL] + r[e]] = p[e] & kMask;
-        lds_barrier();
-
-        // 4. append each chunk to its bin's region
-        const uint32_t tch = wsum[16];
-        for (uint32_t q = tid; q < tch; q += BLOCK) {
-            const uint32_t b = cmap[q];
-            const int32_t d = dst[b];
-            const uint2 e01 = *reinterpret_cast<const uint2*>(ent + 6 * q);
-            const uint2 e23 = *reinterpret_cast<const uint2*>(ent + 6 * q + 2);
-            const uint2 e45 = *reinterpret_cast<const uint2*>(ent + 6 * q + 4);
-            const uint32_t v0 = e01.x;  // a run's chunk always starts with a real entry
-            uint32_t v[6] = {v0, e01.y, e23.x, e23.y, e45.x, e45.y};
-            if (__builtin_expect(d != kRunOvf, 1)) {
-#pragma unroll
-                for (int f = 1; f < 6; f++) v[f] = v[f] == kNoPos ? v0 : v[f];
-                const uint2 w0 = pack3w<SL>(v[0], v[1], v[2]), w1 = pack3w<SL>(v[3], v[4], v[5]);
-                rgn[d + (int32_t)q] = make_uint4(w0.x, w0.y, w1.x, w1.y);
-            } else {
-#pragma unroll
-                for (int f = 0; f < 6; f++)
-                    if (v[f] != kNoPos) or_pos_global<SL>(a.gw, a.b0 + b, v[f]);
-            }
-        }
-    }
-    if (tid < nb) a.counts[(uint64_t)(a.b0 + tid) * gridDim.x + blockIdx.x] = fill[tid];
-}
-
-// Pass B over sorted tiles.  Unit u (bin j of the sweep, or half h of it for
-// 2^21-bit bins) loads its 2^20-bit slice into LDS, ORs in the bin's run of
-// every tile, and writes the slice back.
-// Runs are ~40 entries (C2), ~7 chunks of 16 B, of any alignment: a fixed
-// number of lanes per run leaves most chunk slots idle.  So each wave takes a
-// batch of 64 tiles (one lane each: the run's bounds), scans the runs' chunk
-// counts and writes one dense list of the batch's chunks into its own LDS
-// (entry: tile lane | first / last valid entry of the chunk | chunk index);
-// then lane L applies list entries L, L + 64, ... with R chunk loads in
-// flight.  The next batch's bounds load while this batch applies.
-// XCD-aware unit order: block x runs unit (x % 8) * per + x / 8, so each XCD
-// applies a contiguous range of bins whose runs share cache lines (the run
-// table rows and the runs' edge words) in its own L2.
-template <int SL>
-__global__ __launch_bounds__(kApplyBlock) void k_apply_runs(PassS a, uint32_t* __restrict__ gw, uint64_t nw32) {
-    constexpr uint32_t H = 1u << (SL - kSliceLog2);
-    constexpr uint32_t kMask = (1u << SL) - 1;
-    constexpr uint32_t NWAVE = kApplyBlock / 64;
-    constexpr uint32_t PER = kSliceWords32 / 2 / kApplyBlock;
-    constexpr uint32_t CAP = 512;  // list entries per wave (32 KiB in all)
-    constexpr uint32_t R = 8;      // chunk loads in flight per lane
-    __shared__ uint32_t filt[kSliceWords32];
-    __shared__ uint32_t lists[NWAVE * CAP];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t nunits = a.nb * H;
-    const uint32_t per = (nunits + 7) / 8;
-    const uint32_t u = (blockIdx.x % 8) * per + blockIdx.x / 8;
-    if (u >= nunits) return;  // block-uniform
-    const uint32_t j = u / H, half = u % H;
-    const uint64_t w0 = ((uint64_t)(a.b0 + j) * H + half) * kSliceWords32;
-    if (w0 >= nw32) return;  // the last bin's missing half
-    const uint32_t nw2 = (uint32_t)min((uint64_t)kSliceWords32, nw32 - w0) / 2;
-    uint2* g2 = reinterpret_cast<uint2*>(gw + w0);
-    uint2* f2 = reinterpret_cast<uint2*>(filt);
-    {
-        uint2 v[PER];
-#pragma unroll
-        for (uint32_t q = 0; q < PER; q++) {
-            const uint32_t i = tid + q * kApplyBlock;
-            v[q] = i < nw2 ? g2[i] : make_uint2(0, 0);
-        }
-#pragma unroll
-        for (uint32_t q = 0; q < PER; q++) {
-            const uint32_t i = tid + q * kApplyBlock;
-            if (i < nw2) f2[i] = v[q];
-        }
-    }
-    __syncthreads();
-    uint32_t* list = lists + wave * CAP;
-    auto bounds = [&](uint64_t t, uint32_t& s, uint32_t& e) {
-        s = e = 0;
-        if (t < a.ntiles) {
-            const uint16_t* row = a.runs + t * a.rstride;
-            s = j ? row[j - 1] : 0u;
-            e = row[j];
-        }
-    };
-    uint32_t s, e, acc = 0;
-    bounds((uint64_t)wave * 64 + lane, s, e);
-    for (uint64_t tb = (uint64_t)wave * 64; tb < a.ntiles; tb += 64 * NWAVE) {
-        uint32_t sn, en;
-        bounds(tb + 64 * NWAVE + lane, sn, en);
-        const uint32_t c0 = s / 6;
-        const uint32_t n = e > s ? (e - 1) / 6 - c0 + 1 : 0u;  // chunks of this lane's run
-        uint32_t x = n;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(x, d);
-            if (lane >= (uint32_t)d) x += y;
-        }
-        const uint32_t total = __shfl(x, 63), p0 = x - n;
-        const uint32_t lo0 = s - 6 * c0, hi1 = e - 6 * (c0 + n - 1);  // valid entries [lo, hi) of the end chunks
-        const uint64_t* tbase = a.ents + tb * a.tstride;
-        for (uint32_t base = 0; base < total; base += CAP) {  // wave-uniform; > CAP only for duplicate-heavy runs
-            const uint32_t qa = p0 < base ? base - p0 : 0u;
-            const uint32_t qb = min(n, base + CAP > p0 ? base + CAP - p0 : 0u);
-            for (uint32_t q = qa; q < qb; q++) {
-                const uint32_t lo = q == 0 ? lo0 : 0u, hi = q + 1 == n ? hi1 : 6u;
-                list[p0 + q - base] = lane | (lo << 6) | (hi << 9) | ((c0 + q) << 12);
-            }
-            const uint32_t m = min(CAP, total - base);
-            for (uint32_t r0 = 0; r0 < m; r0 += 64 * R) {
-                uint32_t le[R];
-                uint4 v[R];
-#pragma unroll
-                for (uint32_t i = 0; i < R; i++) {
-                    const uint32_t f = r0 + i * 64 + lane;
-                    le[i] = f < m ? list[f] : 0u;
-                }
-#pragma unroll
-                for (uint32_t i = 0; i < R; i++) {
-                    const uint4* src = reinterpret_cast<const uint4*>(tbase + (uint64_t)(le[i] & 63) * a.tstride);
-                    v[i] = r0 + i * 64 + lane < m && !(LSMB_RABL & 2) ? src[le[i] >> 12] : make_uint4(le[i] * 2654435761u, (le[i] + lane) * 2246822519u, le[i] * 3266489917u, (le[i] ^ 77u) * 668265263u);  // cached: neighbour bins share the edge lines
-                }
-#pragma unroll
-                for (uint32_t i = 0; i < R; i++) {
-                    if (r0 + i * 64 + lane < m) {
-                        const uint32_t lo = (le[i] >> 6) & 7, hi = (le[i] >> 9) & 7;
-                        const uint64_t w0v = ((uint64_t)v[i].y << 32) | v[i].x, w1v = ((uint64_t)v[i].w << 32) | v[i].z;
-#pragma unroll
-                        for (uint32_t f = 0; f < 6; f++) {
-                            const uint32_t o = (uint32_t)((f < 3 ? w0v : w1v) >> (SL * (f % 3))) & kMask;
-                            if (f >= lo && f < hi && (H == 1 || (o >> kSliceLog2) == half)) {
-                                if (LSMB_RABL & 1) acc ^= o; else atomicOr(&filt[(o & kSliceMask) >> 5], 1u << (o & 31));
-                            }
-                        }
-                    }
-                }
-            }
-        }
-        s = sn;
-        e = en;
-    }
-    if (LSMB_RABL & 1) filt[acc & (kSliceWords32 - 1)] |= acc;  // keep the ablated work live
-    __syncthreads();
-    for (uint32_t i = tid; i < nw2; i += kApplyBlock) g2[i] = f2[i];
 }
 
 // ---------------------------------------------------------------- helpers
@@ -1174,130 +739,6 @@ void set_max_lds(const void* fn) {
         if (d == fn) return;
     hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
     done.push_back(fn);
-}
-
-// Sorted-tile partition build (k_sort + k_apply_runs), sweep by sweep: the
-// tile arrays hold one sweep's entries, so each sweep's pass B follows its
-// pass A.  t1 marks the end of the last pass A launched.
-template <class Src>
-hipError_t build_sorted(const Src& src, uint64_t n, const Mod32& md, uint32_t k, uint32_t* gw, uint64_t nw32,
-                        const PartitionPlan& pl, const PartitionWorkspace& ws, hipStream_t st, BuildTimers* tm,
-                        int sweep, bool w32) {
-    for (uint32_t sw = 0; sw < pl.sweeps; sw++) {
-        if (sweep >= 0 && sw != (uint32_t)sweep) continue;
-        PassS a;
-        a.b0 = sw * pl.bins_per_sweep;
-        a.nb = min(pl.bins_per_sweep, pl.nbins - a.b0);
-        a.ntiles = pl.ntiles;
-        a.tstride = pl.tstride;
-        a.rstride = pl.rstride;
-        a.ents = ws.regions;
-        a.runs = reinterpret_cast<uint16_t*>(ws.counts);
-        const bool full = pl.sweeps == 1;
-        auto go = [&](auto kern, uint32_t T) {
-            const size_t smem = kSortLdsFixed + (size_t)T * 4;
-            set_max_lds((const void*)kern);
-            kern<<<dim3(pl.grid), dim3(1024), smem, st>>>(src, n, md, k, a);
-        };
-        auto go7 = [&](auto slc) {  // k = 7 (BloomFilter::new at fpr 0.01): exact k, 5 keys per lane
-            constexpr int SL = decltype(slc)::value;
-            constexpr uint32_t T = 1024 * 5 * 7;
-            if (w32) {
-                if (full) go(k_sort<Src, Walk32, 7, true, true, SL, 1024, 5>, T);
-                else go(k_sort<Src, Walk32, 7, true, false, SL, 1024, 5>, T);
-            } else {
-                if (full) go(k_sort<Src, Walk64, 7, true, true, SL, 1024, 5>, T);
-                else go(k_sort<Src, Walk64, 7, true, false, SL, 1024, 5>, T);
-            }
-        };
-        if (k == 7) {
-            if (pl.slice_log2 == 21) go7(std::integral_constant<int, 21>{});
-            else go7(std::integral_constant<int, kSliceLog2>{});
-        } else if (k <= 8) {
-            if (w32) go(k_sort<Src, Walk32, 8, false, false, kSliceLog2, 1024, 4>, 1024 * 32);
-            else go(k_sort<Src, Walk64, 8, false, false, kSliceLog2, 1024, 4>, 1024 * 32);
-        } else if (k <= 16) {
-            if (w32) go(k_sort<Src, Walk32, 16, false, false, kSliceLog2, 1024, 2>, 1024 * 32);
-            else go(k_sort<Src, Walk64, 16, false, false, kSliceLog2, 1024, 2>, 1024 * 32);
-        } else {
-            if (w32) go(k_sort<Src, Walk32, 32, false, false, kSliceLog2, 1024, 1>, 1024 * 32);
-            else go(k_sort<Src, Walk64, 32, false, false, kSliceLog2, 1024, 1>, 1024 * 32);
-        }
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        if (tm) hipEventRecord(tm->t1, st);
-        const uint32_t H = pl.slice_log2 == 21 ? 2u : 1u;
-        const uint32_t grid = 8 * ((a.nb * H + 7) / 8);
-        if (H == 2)
-            k_apply_runs<21><<<dim3(grid), dim3(kApplyBlock), 0, st>>>(a, gw, nw32);
-        else
-            k_apply_runs<kSliceLog2><<<dim3(grid), dim3(kApplyBlock), 0, st>>>(a, gw, nw32);
-        e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
-}
-
-// Sorted tiles into regions (k_sortr): every sweep's pass A, then one pass B
-// over the requested bins (the regions hold every bin, as with k_bin).
-template <class Src>
-hipError_t build_sortr(const Src& src, uint64_t n, const Mod32& md, uint32_t k, uint32_t* gw, uint64_t nw32,
-                       const PartitionPlan& pl, const PartitionWorkspace& ws, hipStream_t st, BuildTimers* tm,
-                       int sweep, bool w32) {
-    for (uint32_t sw = 0; sw < pl.sweeps; sw++) {
-        if (sweep >= 0 && sw != (uint32_t)sweep) continue;
-        PassR a;
-        a.b0 = sw * pl.bins_per_sweep;
-        a.nb = min(pl.bins_per_sweep, pl.nbins - a.b0);
-        a.nbins = pl.nbins;
-        a.cap = pl.cap_segs;
-        a.ntiles = pl.ntiles;
-        a.regions = ws.regions;
-        a.counts = ws.counts;
-        a.gw = gw;
-        const bool full = pl.sweeps == 1;
-        auto go = [&](auto kern, uint32_t smem) {
-            set_max_lds((const void*)kern);
-            kern<<<dim3(pl.grid), dim3(1024), smem, st>>>(src, n, md, k, a);
-        };
-        auto go7 = [&](auto slc) {  // k = 7 (BloomFilter::new at fpr 0.01): exact k, 4 keys per lane
-            constexpr int SL = decltype(slc)::value;
-            constexpr uint32_t smem = sortr_lds_bytes<4, 7>();
-            if (w32) {
-                if (full) go(k_sortr<Src, Walk32, 7, true, true, SL, 4>, smem);
-                else go(k_sortr<Src, Walk32, 7, true, false, SL, 4>, smem);
-            } else {
-                if (full) go(k_sortr<Src, Walk64, 7, true, true, SL, 4>, smem);
-                else go(k_sortr<Src, Walk64, 7, true, false, SL, 4>, smem);
-            }
-        };
-        if (k == 7) {
-            if (pl.slice_log2 == 21) go7(std::integral_constant<int, 21>{});
-            else go7(std::integral_constant<int, kSliceLog2>{});
-        } else if (k <= 8) {
-            if (w32) go(k_sortr<Src, Walk32, 8, false, false, kSliceLog2, 3>, sortr_lds_bytes<3, 8>());
-            else go(k_sortr<Src, Walk64, 8, false, false, kSliceLog2, 3>, sortr_lds_bytes<3, 8>());
-        } else if (k <= 16) {
-            if (w32) go(k_sortr<Src, Walk32, 16, false, false, kSliceLog2, 1>, sortr_lds_bytes<1, 16>());
-            else go(k_sortr<Src, Walk64, 16, false, false, kSliceLog2, 1>, sortr_lds_bytes<1, 16>());
-        } else {
-            return hipErrorInvalidValue;  // the plan sends k > 16 to the flat tiles
-        }
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
-    if (tm) hipEventRecord(tm->t1, st);
-    const uint32_t bfirst = sweep >= 0 ? (uint32_t)sweep * pl.bins_per_sweep : 0u;
-    const uint32_t bend = sweep >= 0 ? min(pl.nbins, bfirst + pl.bins_per_sweep) : pl.nbins;
-    if (bend > bfirst) {
-        if (pl.slice_log2 == 21)
-            k_apply<21, 1><<<dim3(2 * (bend - bfirst)), dim3(kApplyBlock), 0, st>>>(
-                ws.regions, ws.counts, pl.grid, pl.cap_segs, pl.nbins, gw, nw32, bfirst, bend);
-        else
-            k_apply<kSliceLog2, 1><<<dim3(bend - bfirst), dim3(kApplyBlock), 0, st>>>(
-                ws.regions, ws.counts, pl.grid, pl.cap_segs, pl.nbins, gw, nw32, bfirst, bend);
-    }
-    return hipGetLastError();
 }
 
 template <class Src>
@@ -1364,14 +805,6 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
         const PartitionPlan pl = plan_partition(num_bits, k, n, num_cus);
         if (pl.region_bytes > ws.region_bytes || pl.counts_bytes > ws.counts_bytes) return hipErrorInvalidValue;
         const bool w32 = fits_walk32(num_bits);
-        if (pl.sorted || pl.sortr) {
-            const hipError_t e = pl.sortr ? build_sortr(src, n, md, k, gw, nw32, pl, ws, st, tm, sweep, w32)
-                                          : build_sorted(src, n, md, k, gw, nw32, pl, ws, st, tm, sweep, w32);
-            if (e != hipSuccess || !tm) return e;
-            hipEventRecord(tm->t2, st);
-            tm->valid = true;
-            return hipGetLastError();
-        }
         for (uint32_t sw = 0; sw < pl.sweeps; sw++) {
             if (sweep >= 0 && sw != (uint32_t)sweep) continue;
             PassA a;
@@ -1535,78 +968,7 @@ PartitionPlan plan_partition_sl(uint32_t num_bits, uint32_t k, uint64_t n, int n
 // re-hashes every key) for a second read of each bin's regions in pass B.
 // k = 7 only (the kernels instantiated for it); LSMB_SLICE_LOG2=20 pins 2^20,
 // =21 forces 2^21 (measurement knobs).
-namespace {
-// Sorted-tile plan (k_sort): sweeps of at most kSortMaxBins bins; tiles of
-// 1024 * kpl keys, kpl the most keys per lane whose entries fit LDS.
-PartitionPlan plan_sorted_sl(uint32_t num_bits, uint32_t k, uint64_t n, int num_cus, uint32_t sl) {
-    PartitionPlan pl;
-    pl.sorted = true;
-    pl.slice_log2 = sl;
-    pl.nbins = (uint32_t)(((uint64_t)num_bits + (1ull << sl) - 1) >> sl);
-    pl.sweeps = (pl.nbins + kSortMaxBins - 1) / kSortMaxBins;
-    pl.bins_per_sweep = (pl.nbins + pl.sweeps - 1) / pl.sweeps;
-    const uint32_t kmax = k == 7 ? 7 : k <= 8 ? 8 : k <= 16 ? 16 : 32;
-    pl.kpl = k == 7 ? 5 : 32 / kmax;
-    const uint64_t tk = 1024ull * pl.kpl;
-    const uint32_t T = 1024 * pl.kpl * kmax;
-    pl.ntiles = (n + tk - 1) / tk;
-    pl.tstride = ((T + 2) / 3 + 1) & ~1u;
-    pl.rstride = (pl.bins_per_sweep + 63) & ~63u;
-    uint64_t g = (uint64_t)num_cus;  // one 1024-thread workgroup per CU (LDS)
-    if (g > pl.ntiles) g = pl.ntiles;
-    if (g < 1) g = 1;
-    pl.grid = (uint32_t)g;
-    // a sweep keeps the positions in its bins: the run of one (tile, bin)
-    double keep = (double)pl.bins_per_sweep * (double)(1ull << sl) / (double)num_bits;
-    if (keep > 1.0) keep = 1.0;
-    pl.run_len = (uint32_t)ceil((double)tk * k * keep / pl.bins_per_sweep);
-    pl.region_bytes = pl.ntiles * pl.tstride * 8;
-    pl.counts_bytes = pl.ntiles * pl.rstride * 2;
-    static const bool flat = [] {
-        const char* e = getenv("LSMB_PARTITION");
-        return e && !strcmp(e, "flat");
-    }();
-    if (!flat && k <= 16) {
-        // k_sortr (k <= 16: padded runs and the chunk map must fit LDS next to
-        // the tile): 4 keys per lane for k = 7, 3 for k = 8, 1 for k <= 16;
-        // regions sized for mean + 8 sigma positions plus one padded chunk per tile
-        pl.sortr = true;
-        pl.sorted = false;
-        pl.kpl = k == 7 ? 4 : k <= 8 ? 3 : 1;
-        const uint64_t tk2 = 1024ull * pl.kpl;
-        pl.ntiles = (n + tk2 - 1) / tk2;
-        g = (uint64_t)num_cus;
-        if (g > pl.ntiles) g = pl.ntiles;
-        if (g < 1) g = 1;
-        pl.grid = (uint32_t)g;
-        const uint64_t tiles_w = (pl.ntiles + g - 1) / g;
-        double p = (double)(1ull << sl) / (double)num_bits;
-        if (p > 1.0) p = 1.0;
-        const double mu = (double)(tiles_w * tk2) * k * p;
-        pl.cap_segs = (uint32_t)ceil((mu + 8.0 * sqrt(mu)) / 6.0) + (uint32_t)tiles_w + 2;
-        const bool fits = (uint64_t)pl.nbins * pl.cap_segs < (1ull << 30);
-        pl.region_bytes = fits ? (uint64_t)pl.grid * pl.nbins * pl.cap_segs * 16 : ~0ull >> 2;
-        pl.counts_bytes = (uint64_t)pl.nbins * pl.grid * 4;
-    }
-    return pl;
-}
-}  // namespace
-
 PartitionPlan plan_partition(uint32_t num_bits, uint32_t k, uint64_t n, int num_cus) {
-    // LSMB_PARTITION=flat|sortr: the sorted-tile pass A experiments (DESIGN.md
-    // section 4.2); the default is the per-slice ring pass A (k_bin)
-    static const bool ring = [] {
-        const char* e = getenv("LSMB_PARTITION");
-        return !(e && (!strcmp(e, "flat") || !strcmp(e, "sortr")));
-    }();
-    if (!ring && k <= 32) {
-        const char* e = getenv("LSMB_SLICE_LOG2");  // measurement knobs: =20 pins, =21 forces 2^21-bit bins
-        if (k == 7 && e && atoi(e) == 21 && num_bits > (1u << 21)) return plan_sorted_sl(num_bits, k, n, num_cus, 21);
-        const PartitionPlan s20 = plan_sorted_sl(num_bits, k, n, num_cus, kSliceLog2);
-        if (s20.sweeps < 2 || k != 7 || (e && atoi(e) == 20)) return s20;
-        const PartitionPlan s21 = plan_sorted_sl(num_bits, k, n, num_cus, 21);
-        return s21.sweeps < s20.sweeps ? s21 : s20;
-    }
     const PartitionPlan p20 = plan_partition_sl(num_bits, k, n, num_cus, kSliceLog2);
     const char* e = getenv("LSMB_SLICE_LOG2");
     if (k == 7 && e && atoi(e) == 21 && num_bits > (1u << 21))  // measurement: force 2^21-bit bins

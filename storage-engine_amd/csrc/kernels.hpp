@@ -56,16 +56,8 @@ struct PartitionPlan {
     uint32_t ring = 0;            // pass A ring entries per slice (multiple of 4, >= kSegEntries)
     uint32_t sweeps = 0;
     uint32_t keys_per_lane = 1;   // pass A keys per lane per phase (2: k = 7 sweeps)
-    uint64_t region_bytes = 0;    // nbins * grid * cap_segs * 64 (sorted: ntiles * tstride * 8)
-    uint64_t counts_bytes = 0;    // nbins * grid * 4 (sorted: ntiles * rstride * 2)
-    // Sorted-tile pass A (k_sort; the default): tiles of tile_keys keys, each
-    // written as tstride packed u64 words plus a run-table row of rstride u16.
-    bool sorted = false;          // flat tiles + run table (k_sort / k_apply_runs)
-    bool sortr = false;           // tiles appended to per-(workgroup, bin) regions (k_sortr / k_apply<SL, 1>)
-    uint32_t kpl = 0;             // keys per lane per tile (tile_keys = 1024 * kpl)
-    uint64_t ntiles = 0;
-    uint32_t tstride = 0, rstride = 0;
-    uint32_t run_len = 0;         // expected entries per (tile, bin) run: picks pass B's lanes per run
+    uint64_t region_bytes = 0;    // nbins * grid * cap_segs * 64
+    uint64_t counts_bytes = 0;    // nbins * grid * 4
 };
 
 PartitionPlan plan_partition(uint32_t num_bits, uint32_t k, uint64_t n, int num_cus);

@@ -3,7 +3,7 @@
 # fetch / write, L2 hit / miss, SQ mix) -> gpurun_out/ps_<tag>/
 TAG=${1:-x}; shift || true
 REPO=${GRAFT_REPO_ROOT:-/root/repo}
-OUT=$REPO/gpurun_out/ps_$TAG
+OUT=$REPO/gpurun_out/pq_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 BENCH="$REPO/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-e2e --no-varlen --no-exact10 --no-probe $*"
