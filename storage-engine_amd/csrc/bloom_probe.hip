@@ -382,10 +382,15 @@ __global__ __launch_bounds__(BS) void k_fset_sliced(Src src, uint64_t n, const R
 // filter in L2.  Per key and class with an in-range member: one walk, k
 // table reads ANDed over the class's members; the class's hits map back to
 // descriptor bits; the range mask then keeps the in-range ones.
-constexpr uint32_t kClassBlock = 1024;  // one workgroup per CU shares one copy of the tables
+// Workgroups per CU: two for 16-B keys (registers capped at 64 for 8 waves
+// per SIMD: 62, no spills; mixed set 0.151 -> 0.132 ms), one for the
+// var-len / odd-length sources, which would spill at that cap.
+constexpr uint32_t kClassBlock = 1024;
+template <class Src>
+constexpr uint32_t class_wgs_per_cu() { return std::is_same<Src, ks::Fixed16>::value ? 2u : 1u; }
 
 template <class Src>
-__global__ __launch_bounds__(kClassBlock) void k_fset_classes(Src src, uint64_t n, const RangedFilter* __restrict__ filters,
+__global__ __launch_bounds__(kClassBlock, 4 * class_wgs_per_cu<Src>()) void k_fset_classes(Src src, uint64_t n, const RangedFilter* __restrict__ filters,
                                                       uint32_t nfilt, FsetRanges rg, FsetClasses cl,
                                                       uint64_t* __restrict__ out) {
     extern __shared__ __align__(16) uint8_t smem_raw[];
@@ -437,10 +442,9 @@ __global__ __launch_bounds__(kClassBlock) void k_fset_classes(Src src, uint64_t 
             if (!(rm & C[c].mask)) continue;
             const uint8_t* t = smem_raw + C[c].off;
             const uint32_t width = C[c].width, kc = C[c].k;
-            const Mod32 md = C[c].md;
-            Walk32 pw(md, h.lo, h.hi);
             uint64_t acc = ~0ull;
-            auto walk = [&](auto tag) {  // entry type: uniform per class
+            // entry type and walk (Walk14 below 2^14 bits): uniform per class
+            auto walk = [&](auto tag, auto pw, const auto& md) {
                 using E = decltype(tag);
                 const E* te = reinterpret_cast<const E*>(t);
                 if (kc == 7) {
@@ -456,10 +460,19 @@ __global__ __launch_bounds__(kClassBlock) void k_fset_classes(Src src, uint64_t 
                     }
                 }
             };
-            if (width == 1) walk(uint8_t{});
-            else if (width == 2) walk(uint16_t{});
-            else if (width == 4) walk(uint32_t{});
-            else walk(uint64_t{});
+            auto walk_w = [&](auto pw, const auto& md) {
+                if (width == 1) walk(uint8_t{}, pw, md);
+                else if (width == 2) walk(uint16_t{}, pw, md);
+                else if (width == 4) walk(uint32_t{}, pw, md);
+                else walk(uint64_t{}, pw, md);
+            };
+            if (Mod14::fits(C[c].num_bits)) {
+                const Mod14 md = C[c].md14;
+                walk_w(Walk14(md, h.lo, h.hi), md);
+            } else {
+                const Mod32 md = C[c].md;
+                walk_w(Walk32(md, h.lo, h.hi), md);
+            }
             if (C[c].nmem < 64) acc &= (1ull << C[c].nmem) - 1;
             while (acc) {
                 const uint32_t j = (uint32_t)__builtin_ctzll(acc);
@@ -522,7 +535,7 @@ hipError_t fset_probe_with(const Src& src, uint64_t n, const RangedFilter* df, u
     if (!(shared_nb > 0 && shared_k > 0) && cl.ncls > 0 && cl.table_bytes <= kFsetTableBytes) {
         const size_t smem = cl.table_bytes;
         uint64_t gc = (n + kClassBlock - 1) / kClassBlock;
-        if (gc > (uint64_t)num_cus) gc = (uint64_t)num_cus;
+        if (gc > (uint64_t)num_cus * class_wgs_per_cu<Src>()) gc = (uint64_t)num_cus * class_wgs_per_cu<Src>();
         if (gc < 1) gc = 1;
         hipFuncSetAttribute((const void*)k_fset_classes<Src>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         k_fset_classes<Src><<<dim3((uint32_t)gc), dim3(kClassBlock), smem, st>>>(src, n, df, nfilt, rg, cl, out);

@@ -1044,6 +1044,7 @@ int fset_refresh(lsmb_fset* fs) {
             c.num_bits = (uint32_t)(keyd[a].first >> 32);
             c.k = (uint32_t)keyd[a].first;
             c.md = Mod32::make(c.num_bits);
+            c.md14 = Mod14::make(Mod14::fits(c.num_bits) ? c.num_bits : 1);
             c.nmem = (uint32_t)(b - a);
             c.width = c.nmem <= 8 ? 1 : c.nmem <= 16 ? 2 : c.nmem <= 32 ? 4 : 8;
             for (size_t j = a; j < b; j++) {

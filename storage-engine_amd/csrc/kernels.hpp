@@ -145,6 +145,7 @@ constexpr uint32_t kFsetMaxClasses = 8;
 constexpr uint32_t kFsetTableBytes = 64 * 1024;
 struct FsetClass {
     Mod32 md;
+    Mod14 md14;        // valid when num_bits < 2^14 (small): the walk's cheaper reduction
     uint32_t num_bits, k;
     uint32_t off;      // byte offset of the class table in the LDS tables
     uint32_t width;    // entry bytes: 1, 2, 4 or 8 (members <= 8, 16, 32, 64)
