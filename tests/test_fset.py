@@ -322,3 +322,32 @@ def test_fset_mixed_size_classes(oracle, sizes):
     assert [int(x) for x in got] == expected_masks(oracle, tables, [bytes(r) for r in q])
     fs.close()
     ctx.close()
+
+
+@pytest.mark.gpu
+def test_fset_mixed_size_classes_varlen_keys(oracle):
+    """Mixed-size classes probed with variable-length keys (k_fset_classes'
+    VarLen instance: one workgroup per CU, unlike the 16-B-key instance), a
+    class below 2^14 bits (Mod14 walk) next to bigger ones (Mod32 walk)."""
+    ctx = lsmbloom.Context(0)
+    fs = FilterSet(ctx)
+    data, offs = keygen.varlen(24_000)
+    keys = [bytes(data[offs[i]:offs[i + 1]]) for i in range(24_000)]
+    tables = {}
+    for t, n in enumerate([1000, 4000, 1000, 4000, 30_000, 1000]):
+        mem = keys[t * 3000:t * 3000 + min(n, 3000)]
+        d, o = keygen.pack(mem)
+        nb, k = lsmbloom.params(n, 0.01)
+        w = oracle.build_var(d, o, nb, k)
+        rows = sorted(mem)
+        lo, hi = rows[t % 3 * 10], rows[-1 - t % 2 * 10]
+        s = fs.add_filter(BloomFilter(w, k, nb), lo, hi)
+        tables[s] = (w, nb, k, lo, hi)
+    fs.remove(1)
+    del tables[1]
+    q = keys[:20_000:3] + keys[18_000:]
+    d, o = keygen.pack(q)
+    got = fs.probe(d, offsets=o)
+    assert [int(x) for x in got] == expected_masks(oracle, tables, q)
+    fs.close()
+    ctx.close()
