@@ -741,6 +741,19 @@ void set_max_lds(const void* fn) {
     done.push_back(fn);
 }
 
+// k_hash_var geometry: keys per workgroup and LDS window (measurement knobs
+// LSMB_HV_KEYS / LSMB_HV_WIN; the window is a whole number of 16-B load rounds).
+#ifndef LSMB_HV_KEYS
+#define LSMB_HV_KEYS 256
+#endif
+#ifndef LSMB_HV_WIN
+#define LSMB_HV_WIN (36 * 1024)
+#endif
+void launch_hash_var(const VarLen& src, uint64_t n, uint4* out, hipStream_t st) {
+    const uint64_t g = (n + LSMB_HV_KEYS - 1) / LSMB_HV_KEYS;
+    k_hash_var<0, LSMB_HV_KEYS, LSMB_HV_WIN><<<dim3((uint32_t)g), dim3(LSMB_HV_KEYS), 0, st>>>(src.d, src.o, n, out);
+}
+
 template <class Src>
 hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k, uint32_t* gw,
                       BuildStrategy s, const PartitionWorkspace& ws, int num_cus, hipStream_t st,
@@ -771,7 +784,7 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
             const uint64_t g = (n + 255) / 256;
             if (g > 0x7FFFFFFFull) return hipErrorInvalidValue;
             if constexpr (std::is_same<Src, VarLen>::value)
-                k_hash_var<0><<<dim3((uint32_t)g), dim3(256), 0, st>>>(src.d, src.o, n, ws.hashes);
+                launch_hash_var(src, n, ws.hashes, st);
             else
                 k_hash<Src><<<dim3((uint32_t)g), dim3(256), 0, st>>>(src, n, ws.hashes);
             const Hashed hs{ws.hashes};
@@ -796,7 +809,7 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
         const uint64_t g = (n + 255) / 256;
         if (g > 0x7FFFFFFFull) return hipErrorInvalidValue;
         if constexpr (std::is_same<Src, VarLen>::value)
-            k_hash_var<0><<<dim3((uint32_t)g), dim3(256), 0, st>>>(src.d, src.o, n, ws.hashes);
+            launch_hash_var(src, n, ws.hashes, st);
         else
             k_hash<Src><<<dim3((uint32_t)g), dim3(256), 0, st>>>(src, n, ws.hashes);
         // pass A's timer (t1) covers k_hash + k_bin
