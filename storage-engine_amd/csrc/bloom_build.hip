@@ -937,12 +937,15 @@ PartitionPlan plan_partition_sl(uint32_t num_bits, uint32_t k, uint64_t n, int n
             break;
         }
     }
-    // k = 7 builds take two keys per lane per phase when the ring still
-    // holds a phase's doubled arrivals (LSMB_SWEEP_PER=1 turns it off).
+    // k = 7 sweeps take two keys per lane per phase when the ring still
+    // holds a phase's doubled arrivals (C5 shard: pass A 2.64 -> 2.59 ms).
+    // Single-sweep filters keep one even where the rings would hold two:
+    // it is slower there (4.97e8 bits, 100 M keys: 0.995 -> 1.026 ms).
+    // LSMB_SWEEP_PER=1 / =2 forces one / two (measurement knob).
     if (k == 7) {
         const char* e = getenv("LSMB_SWEEP_PER");
         const uint32_t need2 = (kSegEntries + (uint32_t)ceil(2 * lambda + 2.0 * sqrt(2 * lambda)) + 7) & ~7u;
-        if ((pl.ring >= need2 && !(e && atoi(e) == 1)) || (e && atoi(e) == 2)) pl.keys_per_lane = 2;
+        if ((pl.sweeps > 1 && pl.ring >= need2 && !(e && atoi(e) == 1)) || (e && atoi(e) == 2)) pl.keys_per_lane = 2;
     }
     // 1024-thread workgroups (one resident per CU), at least ~kBinBlock keys
     // each: two per CU for 2^20-bit bins — pass B then streams twice as many,
