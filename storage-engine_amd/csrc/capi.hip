@@ -126,8 +126,10 @@ int build_dev(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k
         return build_dev_ws(c, kb_all, num_bits, k, dw, st, s, sweep);
     // Tiled and partition builds use the context's shared workspace: a build
     // issued on a different stream than the last one waits for it (two
-    // streams' builds would otherwise overwrite each other's regions).
-    if (c->ws_stream) HIP_TRY(hipStreamWaitEvent(st, c->ws_done, 0));
+    // streams' builds would otherwise overwrite each other's regions).  On the
+    // same stream, stream order already serialises them: no wait packet (a
+    // barrier packet between consecutive builds costs the stream ~10 us).
+    if (c->ws_stream && c->ws_stream != st) HIP_TRY(hipStreamWaitEvent(st, c->ws_done, 0));
     const int rc = build_dev_ws(c, kb_all, num_bits, k, dw, st, s, sweep);
     HIP_TRY(hipEventRecord(c->ws_done, st));
     c->ws_stream = st;
