@@ -212,6 +212,12 @@ def main():
         else:
             dist.init_process_group(args.backend)
     ctx = lsmbloom.Context(dev.index)
+    # One explicit stream for all of this rank's work: on torch's default (the
+    # legacy null) stream, the library maps stream NULL to its context's
+    # blocking stream, so each step's words.zero_() and build would sit on
+    # two streams with an implicit synchronisation between every launch
+    # (C2 step 1.500 -> ~1.46 ms on one stream; tools/graph_ab.py).
+    torch.cuda.set_stream(torch.cuda.Stream(dev))
 
     # Workload.  N = 1: C2 (configs[1]), 100 M keys into new(1e8, 0.01).
     # N > 1: C5 (configs[4]), 1e9 keys split over the ranks (strong scaling),

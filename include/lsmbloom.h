@@ -358,7 +358,8 @@ const char* lsmb_build_strategy(uint32_t num_bits, uint32_t num_hashes, uint64_t
 
 /* Timing of the last device build on this context, in milliseconds, per phase
  * (HIP events on the build stream): [0] total, [1] pass A (hash + bin),
- * [2] pass B (apply).  Valid after lsmb_sync. */
+ * [2] pass B (apply).  Waits for the timed build to finish (on whatever
+ * stream it was issued). */
 int lsmb_last_build_ms(lsmb_ctx* ctx, float* out3);
 
 /* Per-build HIP events behind lsmb_last_build_ms: on (1, the default) or off

@@ -885,6 +885,8 @@ int lsmb_last_build_ms(lsmb_ctx* c, float* out3) {
     if (!c || !out3) return fail(LSMB_EINVAL, "null argument");
     if (!c->tm.valid) return fail(LSMB_EINVAL, "no timed build on this context");
     DevGuard g(c->dev);
+    // the build may run on a caller's stream: wait for its end marker, not c->st
+    HIP_TRY(hipEventSynchronize(c->tm.t2));
     HIP_TRY(hipEventElapsedTime(&out3[0], c->tm.t0, c->tm.t2));
     HIP_TRY(hipEventElapsedTime(&out3[1], c->tm.t0, c->tm.t1));
     HIP_TRY(hipEventElapsedTime(&out3[2], c->tm.t1, c->tm.t2));
