@@ -220,16 +220,6 @@ template <class Src, class W, int KMAX, bool EXACT, bool FULL, int PER = 1, int 
 __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md, uint32_t k_, PassA a) {
     static_assert(PER == 1 || EXACT, "two keys per lane: exact k only");
     constexpr uint32_t kMask = (1u << SL) - 1;
-    // Segment format (64 B either way): 24 offsets packed 3 per u64 for
-    // 2^20/2^21-bit bins; 16 raw u32 offsets for 2^22-bit bins (RAW: the ring
-    // slots are the segment, a flush copies them; seg_entries()).
-    constexpr bool RAW = SL >= 22;
-    constexpr uint32_t SEG = seg_entries(SL), SEGB = 4 * SEG;
-    // The sink slice's positions start at nb << SL, which 1024 bins of 2^22
-    // bits put at 2^32: with RAW bins (always one full sweep of <= 2^32 - 1
-    // bits) dead lanes claim on bin 0 with a zero increment instead, and
-    // their slot writes and overflow atomics are skipped by that increment.
-    static_assert(!RAW || FULL, "2^22-bit bins: one sweep");
     constexpr int NP = PER * KMAX;  // positions per lane per phase
     extern __shared__ uint32_t sm[];
     const uint32_t k = EXACT ? (uint32_t)KMAX : k_;
@@ -275,7 +265,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
         if (__builtin_expect(__ballot(!ok) != 0, 0)) {
 #pragma unroll
             for (int q = 0; q < KMAX; q++)
-                if (!ok && (EXACT || (uint32_t)q < k)) out[q] = RAW ? 0u : sink;
+                if (!ok && (EXACT || (uint32_t)q < k)) out[q] = sink;
         }
     };
     // a lane's keys of phase `it`: key_index(it) + j, j < PER
@@ -397,17 +387,16 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
             for (int q = 0; q < NP; q++) {
                 if (EXACT || (uint32_t)q < k) {
                     if (LSMB_ABL & 2) continue;
-                    if (RAW ? kinc[q / KMAX] != 0 : (FULL || pos[q] < sink))
-                        *(uint32_t*)((char*)sm + slot(q)) = pos[q] & kMask;
+                    if (FULL || pos[q] < sink) *(uint32_t*)((char*)sm + slot(q)) = pos[q] & kMask;
                 }
             }
         } else {
 #pragma unroll
             for (int q = 0; q < NP; q++) {
-                if ((EXACT || (uint32_t)q < k) && (RAW ? kinc[q / KMAX] != 0 : (FULL || pos[q] < sink))) {
+                if ((EXACT || (uint32_t)q < k) && (FULL || pos[q] < sink)) {
                     if (got[q] < lim) {
                         *(uint32_t*)((char*)sm + slot(q)) = pos[q] & kMask;
-                    } else if (RAW || pos[q] < sink) {  // (the sink's claims add 0: never past its ring)
+                    } else if (pos[q] < sink) {  // (the sink's claims add 0: never past its ring)
                         or_pos_global<SL>(a.gw, a.b0 + (pos[q] >> SL), pos[q] & kMask);
 #ifdef LSMB_STATS
                         atomicAdd(a.err + 9, 1u);
@@ -447,51 +436,37 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
                 cnt = 0;
             }
         }
-        const bool has = cnt >= SEG;
+        const bool has = cnt >= (uint32_t)kSegEntries;
         const char* ring = (const char*)sm + own * R4;
-        uint4 x0, x1, y0, y1, z0 = make_uint4(0, 0, 0, 0), z1 = make_uint4(0, 0, 0, 0);
+        uint4 x0, x1, y0, y1, z0, z1;
         auto read_segment = [&]() {
-            if constexpr (RAW) {  // 16 entries at start (16 | R: a segment never wraps)
-                x0 = *(const uint4*)(ring + start), x1 = *(const uint4*)(ring + start + 16);
-                y0 = *(const uint4*)(ring + start + 32), y1 = *(const uint4*)(ring + start + 48);
-            } else {
-                // the segment's three 8-entry groups (8 | R: a group never wraps)
-                uint32_t g0 = start, g1 = start + 32, g2 = start + 64;
-                g1 = min(g1, g1 - R4);
-                g2 = min(g2, g2 - R4);
-                x0 = *(const uint4*)(ring + g0), x1 = *(const uint4*)(ring + g0 + 16);
-                y0 = *(const uint4*)(ring + g1), y1 = *(const uint4*)(ring + g1 + 16);
-                z0 = *(const uint4*)(ring + g2), z1 = *(const uint4*)(ring + g2 + 16);
-            }
+            // the segment's three 8-entry groups (8 | R: a group never wraps)
+            uint32_t g0 = start, g1 = start + 32, g2 = start + 64;
+            g1 = min(g1, g1 - R4);
+            g2 = min(g2, g2 - R4);
+            x0 = *(const uint4*)(ring + g0), x1 = *(const uint4*)(ring + g0 + 16);
+            y0 = *(const uint4*)(ring + g1), y1 = *(const uint4*)(ring + g1 + 16);
+            z0 = *(const uint4*)(ring + g2), z1 = *(const uint4*)(ring + g2 + 16);
         };
         auto store_segment = [&](uint32_t off) {
-            if constexpr (RAW) {
-                if (!(LSMB_ABL & 8)) {
-                    __builtin_amdgcn_raw_buffer_store_b128(u32x4{x0.x, x0.y, x0.z, x0.w}, rgn, off, 0, LSMB_STORE_AUX);
-                    __builtin_amdgcn_raw_buffer_store_b128(u32x4{x1.x, x1.y, x1.z, x1.w}, rgn, off + 16, 0, LSMB_STORE_AUX);
-                    __builtin_amdgcn_raw_buffer_store_b128(u32x4{y0.x, y0.y, y0.z, y0.w}, rgn, off + 32, 0, LSMB_STORE_AUX);
-                    __builtin_amdgcn_raw_buffer_store_b128(u32x4{y1.x, y1.y, y1.z, y1.w}, rgn, off + 48, 0, LSMB_STORE_AUX);
-                }
-            } else {
-                const uint2 q0 = pack3w<SL>(x0.x, y0.x, z0.x), q1 = pack3w<SL>(x0.y, y0.y, z0.y);
-                const uint2 q2 = pack3w<SL>(x0.z, y0.z, z0.z), q3 = pack3w<SL>(x0.w, y0.w, z0.w);
-                const uint2 q4 = pack3w<SL>(x1.x, y1.x, z1.x), q5 = pack3w<SL>(x1.y, y1.y, z1.y);
-                const uint2 q6 = pack3w<SL>(x1.z, y1.z, z1.z), q7 = pack3w<SL>(x1.w, y1.w, z1.w);
-                if (!(LSMB_ABL & 8)) {
-                    __builtin_amdgcn_raw_buffer_store_b128(u32x4{q0.x, q0.y, q1.x, q1.y}, rgn, off, 0, LSMB_STORE_AUX);
-                    __builtin_amdgcn_raw_buffer_store_b128(u32x4{q2.x, q2.y, q3.x, q3.y}, rgn, off + 16, 0, LSMB_STORE_AUX);
-                    __builtin_amdgcn_raw_buffer_store_b128(u32x4{q4.x, q4.y, q5.x, q5.y}, rgn, off + 32, 0, LSMB_STORE_AUX);
-                    __builtin_amdgcn_raw_buffer_store_b128(u32x4{q6.x, q6.y, q7.x, q7.y}, rgn, off + 48, 0, LSMB_STORE_AUX);
-                }
+            const uint2 q0 = pack3w<SL>(x0.x, y0.x, z0.x), q1 = pack3w<SL>(x0.y, y0.y, z0.y);
+            const uint2 q2 = pack3w<SL>(x0.z, y0.z, z0.z), q3 = pack3w<SL>(x0.w, y0.w, z0.w);
+            const uint2 q4 = pack3w<SL>(x1.x, y1.x, z1.x), q5 = pack3w<SL>(x1.y, y1.y, z1.y);
+            const uint2 q6 = pack3w<SL>(x1.z, y1.z, z1.z), q7 = pack3w<SL>(x1.w, y1.w, z1.w);
+            if (!(LSMB_ABL & 8)) {
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{q0.x, q0.y, q1.x, q1.y}, rgn, off, 0, LSMB_STORE_AUX);
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{q2.x, q2.y, q3.x, q3.y}, rgn, off + 16, 0, LSMB_STORE_AUX);
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{q4.x, q4.y, q5.x, q5.y}, rgn, off + 32, 0, LSMB_STORE_AUX);
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{q6.x, q6.y, q7.x, q7.y}, rgn, off + 48, 0, LSMB_STORE_AUX);
             }
         };
         auto spill_segment = [&]() {  // region full (adversarial inputs): exact global atomics
             const uint32_t vals[24] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w,
                                        y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w,
                                        z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
-            for (uint32_t t = 0; t < SEG; t++) or_pos_global<SL>(a.gw, a.b0 + own, vals[t]);  // RAW: x0..y1
+            for (int t = 0; t < 24; t++) or_pos_global<SL>(a.gw, a.b0 + own, vals[t]);
 #ifdef LSMB_STATS
-            atomicAdd(a.err + 7, SEG);
+            atomicAdd(a.err + 7, 24u);
 #endif
         };
         // 1. post jobs (owner lanes with a full segment and room in the region)
@@ -507,7 +482,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
                 g1 = min(g1, g1 - R4);
                 g2 = min(g2, g2 - R4);
                 jobtab[wave * kBinJobsPerWave + j] =
-                    make_uint4(rb + start, RAW ? 0u : rb + g1, RAW ? 0u : rb + g2, ((a.b0 + own) * a.cap + segs) * 64u);
+                    make_uint4(rb + start, rb + g1, rb + g2, ((a.b0 + own) * a.cap + segs) * 64u);
                 posted = true;
             }
         }
@@ -522,18 +497,12 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
             uint2 w0 = make_uint2(0, 0), w1 = make_uint2(0, 0);
             if (j < jobs) {
                 const uint4 jb = jobtab[wave * kBinJobsPerWave + j];
-                if constexpr (RAW) {  // entries 4l..4l+3 as they are
-                    const uint4 e = *(const uint4*)((const char*)sm + jb.x + 16 * l);
-                    w0 = make_uint2(e.x, e.y);
-                    w1 = make_uint2(e.z, e.w);
-                } else {
-                    // segment word 2l+e = pack3<SL>(group0[2l+e], group1[2l+e], group2[2l+e])
-                    const uint2 a0 = *(const uint2*)((const char*)sm + jb.x + 8 * l);
-                    const uint2 a1 = *(const uint2*)((const char*)sm + jb.y + 8 * l);
-                    const uint2 a2 = *(const uint2*)((const char*)sm + jb.z + 8 * l);
-                    w0 = pack3w<SL>(a0.x, a1.x, a2.x);
-                    w1 = pack3w<SL>(a0.y, a1.y, a2.y);
-                }
+                // segment word 2l+e = pack3<SL>(group0[2l+e], group1[2l+e], group2[2l+e])
+                const uint2 a0 = *(const uint2*)((const char*)sm + jb.x + 8 * l);
+                const uint2 a1 = *(const uint2*)((const char*)sm + jb.y + 8 * l);
+                const uint2 a2 = *(const uint2*)((const char*)sm + jb.z + 8 * l);
+                w0 = pack3w<SL>(a0.x, a1.x, a2.x);
+                w1 = pack3w<SL>(a0.y, a1.y, a2.y);
                 off = (LSMB_ABL & 16) ? kDrop : jb.w + 16 * l;
             }
             if (!(LSMB_ABL & 8)) __builtin_amdgcn_raw_buffer_store_b128(u32x4{w0.x, w0.y, w1.x, w1.y}, rgn, off, 0, LSMB_STORE_AUX);
@@ -547,8 +516,8 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
                 else
                     spill_segment();
             }
-            const uint32_t nf = cnt / SEG;
-            uint32_t s = start + SEGB;
+            const uint32_t nf = cnt / (uint32_t)kSegEntries;
+            uint32_t s = start + 96;
             start = min(s, s - R4);
             segs = min(segs + 1, a.cap);
             // more full segments (filters with few, busy slices)
@@ -558,11 +527,11 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
                     store_segment(((a.b0 + own) * a.cap + segs) * 64u);
                 else
                     spill_segment();
-                s = start + SEGB;
+                s = start + 96;
                 start = min(s, s - R4);
                 segs = min(segs + 1, a.cap);
             }
-            const uint32_t rem = cnt - nf * SEG;
+            const uint32_t rem = cnt - nf * (uint32_t)kSegEntries;
             fill[own] = (start + 4 * rem) | (rem << 16);
         }
         lds_barrier();
@@ -591,23 +560,18 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
     if (owner) {
         uint32_t cnt = min(fill[own] >> 16, R);
         while (cnt) {
-            const uint32_t m = min(cnt, SEG);
-            uint32_t v[SEG];
+            const uint32_t m = min(cnt, (uint32_t)kSegEntries);
+            uint32_t v[kSegEntries];
 #pragma unroll
-            for (int t = 0; t < (int)SEG; t++) {
+            for (int t = 0; t < kSegEntries; t++) {
                 uint32_t s = start + 4 * ((uint32_t)t < m ? t : 0);
                 s = min(s, s - R4);
                 v[t] = *(const uint32_t*)((const char*)sm + own * R4 + s);
             }
             if (segs < a.cap) {
                 uint64_t* dst = region_ptr(a, a.b0 + own, w) + (uint64_t)segs * kSegWords;
-                if constexpr (RAW) {
 #pragma unroll
-                    for (int t = 0; t < (int)SEG; t++) reinterpret_cast<uint32_t*>(dst)[t] = v[t];
-                } else {
-#pragma unroll
-                    for (int t = 0; t < kSegWords; t++) dst[t] = pack3<SL>(v[t], v[t + 8], v[t + 16]);
-                }
+                for (int t = 0; t < kSegWords; t++) dst[t] = pack3<SL>(v[t], v[t + 8], v[t + 16]);
                 segs++;
             } else {
                 for (uint32_t t = 0; t < m; t++) or_pos_global<SL>(a.gw, a.b0 + own, v[t]);
@@ -693,15 +657,6 @@ __global__ __launch_bounds__(kApplyBlock) void k_apply(const uint64_t* __restric
 #pragma unroll
                 for (uint32_t u = 0; u < U; u++) {
                     if (i0 + u * 64 + lane < n16) {
-                        if constexpr (SL >= 22) {  // raw u32 entries, 4 per piece
-                            const uint32_t e4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                            for (int e = 0; e < 4; e++) {
-                                const uint32_t o = e4[e] & kMask;
-                                if ((o >> kSliceLog2) == half) atomicOr(&filt[(o & kSliceMask) >> 5], 1u << (o & 31));
-                            }
-                            continue;
-                        }
                         const uint64_t lo = ((uint64_t)v[u].y << 32) | v[u].x;
                         const uint64_t hi = ((uint64_t)v[u].w << 32) | v[u].z;
 #pragma unroll
@@ -885,10 +840,7 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
             auto go7 = [&](auto slc) {  // k = 7 (BloomFilter::new at fpr 0.01), bin width 2^SL
                 constexpr int SL = decltype(slc)::value;
                 const bool two = pl.keys_per_lane == 2;
-                if constexpr (SL >= 22) {  // 2^22-bit bins: the plan takes them for one full sweep only
-                    if (w32) go(k_bin<Src, Walk32, 7, true, true, 1, SL>);
-                    else go(k_bin<Src, Walk64, 7, true, true, 1, SL>);
-                } else if (w32) {
+                if (w32) {
                     if (full && two) go(k_bin<Src, Walk32, 7, true, true, 2, SL>);
                     else if (full) go(k_bin<Src, Walk32, 7, true, true, 1, SL>);
                     else if (two) go(k_bin<Src, Walk32, 7, true, false, 2, SL>);
@@ -901,8 +853,7 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
                 }
             };
             if (k == 7) {
-                if (pl.slice_log2 == 22) go7(std::integral_constant<int, 22>{});
-                else if (pl.slice_log2 == 21) go7(std::integral_constant<int, 21>{});
+                if (pl.slice_log2 == 21) go7(std::integral_constant<int, 21>{});
                 else go7(std::integral_constant<int, kSliceLog2>{});
             } else if (k <= 8) {
                 if (w32) go(k_bin<Src, Walk32, 8, false, false>); else go(k_bin<Src, Walk64, 8, false, false>);
@@ -918,10 +869,7 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
         const uint32_t bfirst = sweep >= 0 ? (uint32_t)sweep * pl.bins_per_sweep : 0u;
         const uint32_t bend = sweep >= 0 ? min(pl.nbins, bfirst + pl.bins_per_sweep) : pl.nbins;
         if (bend > bfirst) {
-            if (pl.slice_log2 == 22)
-                k_apply<22><<<dim3(4 * (bend - bfirst)), dim3(kApplyBlock), 0, st>>>(
-                    ws.regions, ws.counts, pl.grid, pl.cap_segs, pl.nbins, gw, nw32, bfirst, bend);
-            else if (pl.slice_log2 == 21)
+            if (pl.slice_log2 == 21)
                 k_apply<21><<<dim3(2 * (bend - bfirst)), dim3(kApplyBlock), 0, st>>>(
                     ws.regions, ws.counts, pl.grid, pl.cap_segs, pl.nbins, gw, nw32, bfirst, bend);
             else
@@ -973,10 +921,8 @@ PartitionPlan plan_partition_sl(uint32_t num_bits, uint32_t k, uint64_t n, int n
     // ring that holds a segment's worth of leftovers plus a phase's arrivals
     // with margin.  Claims past the ring fall back to exact global atomics.
     const double lambda = (double)kBinBlock * k * fmin(1.0, (double)(1u << sl) / (double)num_bits);
-    const uint32_t seg = seg_entries((int)sl);
-    const uint32_t ralign = sl >= 22 ? 15u : 7u;  // rings a multiple of a segment (raw) or of an 8-entry group
-    uint32_t need = seg + (uint32_t)ceil(lambda + 2.0 * sqrt(lambda));
-    need = (need + ralign) & ~ralign;
+    uint32_t need = kSegEntries + (uint32_t)ceil(lambda + 2.0 * sqrt(lambda));
+    need = (need + 7) & ~7u;
     if (need > kMaxRing) need = kMaxRing;
     // Fewest sweeps whose slices fit LDS with that ring; each sweep re-reads
     // and re-hashes the keys and keeps only its own slices' positions.
@@ -984,7 +930,7 @@ PartitionPlan plan_partition_sl(uint32_t num_bits, uint32_t k, uint64_t n, int n
     for (;; pl.sweeps++) {
         pl.bins_per_sweep = (pl.nbins + pl.sweeps - 1) / pl.sweeps;
         uint32_t r = (kBinLdsBudget / (pl.bins_per_sweep + 1) - kBinExtraBytes) / 4;  // + the sink slice
-        r &= ~ralign;
+        r &= ~7u;
         if (r > kMaxRing) r = kMaxRing;
         if (r >= need || pl.bins_per_sweep == 1) {
             pl.ring = r;
@@ -998,7 +944,7 @@ PartitionPlan plan_partition_sl(uint32_t num_bits, uint32_t k, uint64_t n, int n
     // LSMB_SWEEP_PER=1 / =2 forces one / two (measurement knob).
     if (k == 7) {
         const char* e = getenv("LSMB_SWEEP_PER");
-        const uint32_t need2 = (seg + (uint32_t)ceil(2 * lambda + 2.0 * sqrt(2 * lambda)) + ralign) & ~ralign;
+        const uint32_t need2 = (kSegEntries + (uint32_t)ceil(2 * lambda + 2.0 * sqrt(2 * lambda)) + 7) & ~7u;
         if ((pl.sweeps > 1 && pl.ring >= need2 && !(e && atoi(e) == 1)) || (e && atoi(e) == 2)) pl.keys_per_lane = 2;
     }
     // 1024-thread workgroups (one resident per CU), at least ~kBinBlock keys
@@ -1021,8 +967,8 @@ PartitionPlan plan_partition_sl(uint32_t num_bits, uint32_t k, uint64_t n, int n
     double p = (double)(1u << sl) / (double)num_bits;
     if (p > 1.0) p = 1.0;
     const double mu = (double)keys_w * k * p;
-    const double cap_e = mu + 8.0 * sqrt(mu) + 2.0 * seg;
-    pl.cap_segs = (uint32_t)ceil(cap_e / seg);
+    const double cap_e = mu + 8.0 * sqrt(mu) + 2.0 * kSegEntries;
+    pl.cap_segs = (uint32_t)ceil(cap_e / kSegEntries);
     // A region holds at most kMaxRegionSegs segments
     // a bigger plan is reported as unbounded so callers chunk the keys.
     // (and a workgroup's regions within pass A's 2^31-byte buffer range)
@@ -1041,10 +987,6 @@ PartitionPlan plan_partition_sl(uint32_t num_bits, uint32_t k, uint64_t n, int n
 PartitionPlan plan_partition(uint32_t num_bits, uint32_t k, uint64_t n, int num_cus) {
     const PartitionPlan p20 = plan_partition_sl(num_bits, k, n, num_cus, kSliceLog2);
     const char* e = getenv("LSMB_SLICE_LOG2");
-    if (k == 7 && e && atoi(e) == 22 && num_bits > (1u << 22)) {  // measurement: force 2^22-bit bins
-        const PartitionPlan p22 = plan_partition_sl(num_bits, k, n, num_cus, 22);
-        if (p22.sweeps == 1) return p22;  // (k_bin's raw-segment form runs one full sweep only)
-    }
     if (k == 7 && e && atoi(e) == 21 && num_bits > (1u << 21))  // measurement: force 2^21-bit bins
         return plan_partition_sl(num_bits, k, n, num_cus, 21);
     if (p20.sweeps < 2 || k != 7) return p20;

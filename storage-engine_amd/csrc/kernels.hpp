@@ -12,10 +12,7 @@ namespace lsmb {
 constexpr int kSliceLog2 = 20;                        // 2^20 bits = 128 KiB LDS slice
 constexpr uint32_t kSliceWords32 = 1u << (kSliceLog2 - 5);
 constexpr uint32_t kSliceMask = (1u << kSliceLog2) - 1;
-constexpr int kSegEntries = 24;                       // 20/21-bit offsets per 64-B segment (3 per u64)
-// Offsets per 64-B segment for a bin width of 2^sl bits: 24 packed 3 per u64
-// (sl = 20, 21); 16 raw u32 (sl = 22, whose 22-bit offsets do not pack 3 per u64).
-constexpr uint32_t seg_entries(int sl) { return sl >= 22 ? 16u : (uint32_t)kSegEntries; }
+constexpr int kSegEntries = 24;                       // 20-bit offsets per 64-B segment
 constexpr int kSegWords = 8;                          // 3 offsets per u64 word
 constexpr int kBinBlock = 1024;                       // pass A workgroup
 constexpr int kApplyBlock = 1024;                     // pass B workgroup

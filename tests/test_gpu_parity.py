@@ -494,25 +494,3 @@ def test_c4_full_size_properties(ctx, oracle):
         assert f.may_contain(key)
     del data, offs, mono
     torch.cuda.empty_cache()
-
-
-@pytest.mark.parametrize("n,filter_keys,shape", [
-    (20_000_000, 10**9, "key16"),      # C5's filter in one sweep of 1024 2^22-bit bins
-    (8_000_000, 10**8, "key16"),       # C2's filter as 229 bins
-    (3_000_000, 10**9, "dup"),         # half the keys one key: ring overflow + full regions (spill)
-    (2_000_000, 10**9, "var"),         # var-len keys (pre-hashed pass A)
-])
-def test_build_22bit_bins_raw_segments(ctx, oracle, monkeypatch, n, filter_keys, shape):
-    """2^22-bit bins (LSMB_SLICE_LOG2=22): raw u32 offsets in 16-entry
-    segments, pass B in four 2^20-bit quarters; every word vs the oracle."""
-    monkeypatch.setenv("LSMB_SLICE_LOG2", "22")
-    nb, k = lsmbloom.params(filter_keys, 0.01)
-    assert lsmbloom.build_sweeps(nb, n, k) == 1
-    if shape == "var":
-        data, offs = keygen.varlen(n)
-        _cmp(ctx.build_var(data, offs, nb, k), oracle.build_var_mt(data, offs, nb, k, 16))
-        return
-    keys = keygen.key16(0x5EED2222, 0, n)
-    if shape == "dup":
-        keys[: n // 2] = keys[0]
-    _cmp(ctx.build_fixed(keys, 16, nb, k), oracle.build_fixed_mt(keys, 16, nb, k, 16))
