@@ -101,15 +101,54 @@ def cpu_model():
     return "unknown"
 
 
+def host_cpus():
+    """The host CPUs this process may run on: sched_getaffinity, capped by a
+    cgroup CPU quota if one is set; with the physical cores behind them
+    (distinct (physical id, core id) of /proc/cpuinfo) and the CPU model."""
+    aff = sorted(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = max(1, q // per)
+        except (OSError, ValueError):
+            pass
+    cores, cur = set(), {}
+    try:
+        for line in open("/proc/cpuinfo"):
+            if ":" in line:
+                k, v = (x.strip() for x in line.split(":", 1))
+                cur[k] = v
+            elif cur:
+                if int(cur.get("processor", -1)) in aff:
+                    cores.add((cur.get("physical id"), cur.get("core id")))
+                cur = {}
+        if cur and int(cur.get("processor", -1)) in aff:
+            cores.add((cur.get("physical id"), cur.get("core id")))
+    except (OSError, ValueError):
+        pass
+    use = min(len(aff), quota) if quota else len(aff)
+    return {"threads": max(1, use), "affinity_cpus": len(aff), "cgroup_cpu_quota": quota,
+            "physical_cores": len(cores) or None, "cpu": cpu_model()}
+
+
 def cpu_baseline(num_bits, k, budget_s):
-    """Oracle (C restatement of src/bloom) on the box's host cores, reported
-    beside the GPU numbers: the C2-size filter built from the
-    first S keys of the same workload (S grown until ~budget_s, 1 thread, and
-    all cores with atomic fetch_or), and C1 (configs[0]): build + probe of
-    100 k 16-B keys, 1 thread and all cores."""
+    """Oracle (C restatement of src/bloom, built on this host with -O3
+    -march=native: BASELINE.md) on the box's host cores, reported beside the
+    GPU numbers: the C2-size filter built from the first S keys of the same
+    workload (S grown until ~budget_s, 1 thread; then every host CPU this
+    process may use, with atomic fetch_or), and C1 (configs[0]): build + probe
+    of 100 k 16-B keys, 1 thread and all of those CPUs."""
     import numpy as np
     import oracle_ct
-    orc = oracle_ct.load()
+    orc, how = oracle_ct.load_native()
+    hc = host_cpus()
     words = np.zeros((num_bits + 63) // 64, dtype=np.uint64)
     done, t_used, chunk = 0, 0.0, 1_000_000
     keys = None
@@ -119,19 +158,24 @@ def cpu_baseline(num_bits, k, budget_s):
         orc.build_fixed(keys, 16, num_bits, k, words=words)
         t_used += time.perf_counter() - t0
         done += chunk
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    threads = hc["threads"]
     st = {"value": round(done / t_used / 1e6, 3), "unit": "Mkeys/s", "cores": 1, "kind": "port",
-          "cpu": cpu_model(), "host_threads_available": threads,
+          "cpu": hc["cpu"], "host": hc, "oracle_build": how,
           "sample": "first %d keys of the C2 workload into the full C2 filter (%d bits, k=%d), "
-                    "1 thread, oracle/bloom_oracle.c -O3" % (done, num_bits, k)}
+                    "1 thread, %s" % (done, num_bits, k, how)}
     words[:] = 0
-    n_mt = min(done * threads, 20_000_000)
+    n_mt = min(max(done * threads // 4, 4_000_000), 100_000_000)
     keys = orc.key16(SEED_MEMBERS, 0, n_mt)
+    orc.build_fixed_mt(keys[:1_000_000], 16, num_bits, k, threads, words=words)  # warm-up: threads, pages
+    words[:] = 0
     t0 = time.perf_counter()
     orc.build_fixed_mt(keys, 16, num_bits, k, threads, words=words)
     dt = time.perf_counter() - t0
     st["multi_thread"] = {"value": round(n_mt / dt / 1e6, 3), "cores": threads,
-                          "sample": "first %d keys, atomic fetch_or" % n_mt}
+                          "sample": "first %d keys, atomic fetch_or, %d threads = every CPU this process may use "
+                                    "(affinity %d, cgroup quota %s; %s physical cores)"
+                                    % (n_mt, threads, hc["affinity_cpus"], hc["cgroup_cpu_quota"],
+                                       hc["physical_cores"])}
     st["c1"] = cpu_c1(orc, threads)
     return st
 
@@ -789,6 +833,11 @@ def bench_probe(ctx, dev, args, world=1, rank=0, max_over_ranks=lambda x: x):
                        % (Q_all, F, nb, k, ", %d per GPU" % Q if world > 1 else ""),
            "value": round(Q * world / (ms * 1e-3) / 1e6, 2), "unit": "Mkeys/s", "ms": round(ms, 4),
            "achieved_GBs": round(alg / (ms * 1e-3) / 1e9, 1), "member_rows_all_hit": hits == Q // 2}
+    # Every answer of the full-size run against the oracle's (digests committed
+    # in tests/golden/c3_fixture.json by gen_c3_fixture.py; outside the timing).
+    c3fx = c3_fixture() if world == 1 else None
+    if c3fx and c3fx["Q"] == Q and c3fx["F"] == F:
+        res["answers_equal_oracle_fixture"] = _sha(out) == c3fx["probe_mask_sha256"]
     # The same batch through the device-resident filter set (lsmb_fset): per
     # key and SSTable, min_key <= key <= max_key && may_contain — the checks
     # SSTable::get makes (src/sstable/reader.rs:192-199) — for all 8 tables.
@@ -814,6 +863,8 @@ def bench_probe(ctx, dev, args, world=1, rank=0, max_over_ranks=lambda x: x):
     res["fset"] = {"what": "lsmb_fset_probe_dev: range pre-check + bloom, %d tables, u64 mask per key" % F,
                    "value": round(Q * world / (fms * 1e-3) / 1e6, 2), "unit": "Mkeys/s", "ms": round(fms, 4),
                    "member_rows_own_table_hit": bool(own.all().item())}
+    if c3fx and c3fx["Q"] == Q and c3fx["F"] == F:
+        res["fset"]["answers_equal_oracle_fixture"] = _sha(fout) == c3fx["fset_mask_sha256"]
     fs.close()
     # Mixed sizes: 4 of the C3 tables next to 4 compaction-sized ones
     # (new(4000, 0.01), 38 271 bits): two (num_bits, k) classes, each its own
@@ -845,8 +896,21 @@ def bench_probe(ctx, dev, args, world=1, rank=0, max_over_ranks=lambda x: x):
     res["fset_mixed"] = {"what": "lsmb_fset_probe_dev, %d tables of two sizes: %d x new(1000, 0.01) + %d x "
                                  "new(4000, 0.01), one LDS table per size class" % (F, F // 2, F - F // 2),
                          "value": round(Q * world / (mms * 1e-3) / 1e6, 2), "unit": "Mkeys/s", "ms": round(mms, 4)}
+    if c3fx and c3fx["Q"] == Q and c3fx["F"] == F:
+        res["fset_mixed"]["answers_equal_oracle_fixture"] = _sha(fout) == c3fx["fset_mixed_mask_sha256"]
     fs.close()
     return res
+
+
+def c3_fixture():
+    p = os.path.join(ROOT, "tests", "golden", "c3_fixture.json")
+    return json.load(open(p)) if os.path.exists(p) else None
+
+
+def _sha(t):
+    """sha256 of a device tensor's bytes (little-endian, row-major)."""
+    import hashlib
+    return hashlib.sha256(t.contiguous().cpu().numpy().tobytes()).hexdigest()
 
 
 if __name__ == "__main__":

@@ -79,32 +79,19 @@ hipStream_t pick_stream(lsmb_ctx* c, void* stream) {
     return stream ? reinterpret_cast<hipStream_t>(stream) : c->st;
 }
 
-// Reads (and clears) the kernels' device error flag.  Requires the work that
-// could set it to have completed.
-int check_device_error(lsmb_ctx* c) {
+// LSMB_STATS builds only (diagnostics, never the product): pass A counts the
+// positions that went past a ring or a full region to exact global atomics.
+void report_stats(lsmb_ctx* c) {
 #ifdef LSMB_STATS
-    {
-        uint32_t st[16];
-        HIP_TRY(hipMemcpy(st, c->err.p, 64, hipMemcpyDeviceToHost));
-        fprintf(stderr, "[lsmb stats] ring_overflow=%u region_full=%u\n", st[9], st[7]);
-        HIP_TRY(hipMemset((char*)c->err.p + 4, 0, 60));
-    }
+    uint32_t st[16];
+    if (hipMemcpyAsync(st, c->err.p, 64, hipMemcpyDeviceToHost, c->st) != hipSuccess ||
+        hipStreamSynchronize(c->st) != hipSuccess)
+        return;
+    fprintf(stderr, "[lsmb stats] ring_overflow=%u region_full=%u\n", st[9], st[7]);
+    (void)hipMemsetAsync(c->err.p, 0, 64, c->st);
+#else
+    (void)c;
 #endif
-    // Only the partition kernels set the flag: skip the readback (a sync
-    // round trip) after builds that ran none.
-    if (!c->ran_partition) return LSMB_OK;
-    c->ran_partition = false;
-    HIP_TRY(hipMemcpyAsync(c->err_host, c->err.p, 32, hipMemcpyDeviceToHost, c->st));
-    HIP_TRY(hipStreamSynchronize(c->st));
-    if (*c->err_host) {
-        uint32_t e[8];
-        memcpy(e, c->err_host, 32);
-        HIP_TRY(hipMemsetAsync(c->err.p, 0, 32, c->st));
-        HIP_TRY(hipStreamSynchronize(c->st));
-        return fail(LSMB_EHIP, "partition build: bounded wait timed out (internal error, code %u, diag %u %u %u %u)",
-                    e[0], e[1], e[2], e[3], e[4]);
-    }
-    return LSMB_OK;
 }
 
 namespace {
@@ -158,7 +145,6 @@ int build_dev_ws(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_
                              c->timing ? &c->tm : nullptr, sweep));
         return LSMB_OK;
     }
-    c->ran_partition = true;
     uint64_t chunk = partition_chunk_keys(num_bits, k, workspace_limit_bytes(), c->num_cus);
     if (chunk == 0) return fail(LSMB_ENOMEM, "partition workspace limit too small");
     chunk = std::min(chunk, kb_all.n);
@@ -250,7 +236,7 @@ int host_build_small(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, 
     const uint64_t kpad = (kbytes + 15) & ~15ull, opad = (obytes + 15) & ~15ull;
     const uint64_t need = kpad + opad + nw * 8 + 64;
     if (c->pin_small_cap < need) {
-        if (c->pin_small) HIP_TRY(hipHostFree(c->pin_small));
+        c->pinned_retired.retire(c->pin_small);  // a D2H of an earlier call may not have left it
         c->pin_small = nullptr;
         c->pin_small_cap = 0;
         const uint64_t cap = std::max<uint64_t>(need, kSmallHostBuild + 64);
@@ -284,7 +270,7 @@ int host_build_small(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, 
     HIP_TRY(hipMemcpyAsync(pw, dw, nw * 8, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(hipStreamSynchronize(c->st));
     memcpy(words_out, pw, nw * 8);
-    return check_device_error(c);
+    return LSMB_OK;
 }
 
 int host_build_dev(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
@@ -318,7 +304,7 @@ int host_build_dev(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, ui
         if (bytes) HIP_TRY(hipMemcpyAsync(c->kslot[s].p, data + base, bytes, hipMemcpyHostToDevice, c->cst));
         if (offsets) {
             if (c->offs_pin_cap[s] < m + 1) {
-                if (c->offs_pin[s]) HIP_TRY(hipHostFree(c->offs_pin[s]));
+                c->pinned_retired.retire(c->offs_pin[s]);
                 c->offs_pin[s] = nullptr;
                 c->offs_pin_cap[s] = 0;
                 const uint64_t cap = std::max<uint64_t>(m + 1, std::min<uint64_t>(n, max_keys) + 1);
@@ -366,7 +352,7 @@ int host_build(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, uint32
         if (int rc = crc32_dev(c, (const uint8_t*)dw, nw * 8, *crc, c->st, crc)) return rc;
     }
     HIP_TRY(hipStreamSynchronize(c->st));
-    return check_device_error(c);
+    return LSMB_OK;
 }
 
 // The library's own host build: BloomFilter::insert per key
@@ -540,10 +526,9 @@ int lsmb_open(lsmb_ctx** out, int device) {
         return fail(LSMB_ENODEV, "stream/event creation failed on device %d", device);
     }
     if (c->err.ensure(64) != hipSuccess || hipMemsetAsync(c->err.p, 0, 64, c->st) != hipSuccess ||
-        hipStreamSynchronize(c->st) != hipSuccess ||
-        hipHostMalloc((void**)&c->err_host, 64, 0) != hipSuccess) {
+        hipStreamSynchronize(c->st) != hipSuccess) {
         lsmb_close(c);
-        return fail(LSMB_ENOMEM, "error-flag allocation failed on device %d", device);
+        return fail(LSMB_ENOMEM, "counter allocation failed on device %d", device);
     }
     *out = c;
     return LSMB_OK;
@@ -554,24 +539,24 @@ void lsmb_close(lsmb_ctx* c) {
     {
         DevGuard g(c->dev);
         hipStreamSynchronize(c->st);
-        if (c->err_host) hipHostFree(c->err_host);
         if (c->cst) hipStreamSynchronize(c->cst);
-        for (DevBuf* b : {&c->ws_regions, &c->ws_counts, &c->ws_hashes, &c->err, &c->keys, &c->offs, &c->words, &c->out,
+        for (DevBuf* b : {&c->ws_regions, &c->ws_counts, &c->ws_hashes, &c->crc_parts, &c->err, &c->keys, &c->offs, &c->words, &c->out,
                           &c->filt_words, &c->filt_desc, &c->kslot[0], &c->kslot[1], &c->oslot[0], &c->oslot[1]})
             b->release();
         for (int s = 0; s < 2; s++) {
-            if (c->offs_pin[s]) hipHostFree(c->offs_pin[s]);
+            if (c->offs_pin[s]) hipHostFree(c->offs_pin[s]);  // teardown
             if (c->ev_copy[s]) hipEventDestroy(c->ev_copy[s]);
             if (c->ev_built[s]) hipEventDestroy(c->ev_built[s]);
         }
         if (c->cst) hipStreamDestroy(c->cst);
-        if (c->pin_small) hipHostFree(c->pin_small);
+        if (c->pin_small) hipHostFree(c->pin_small);  // teardown
+        c->pinned_retired.release();
         hipEventDestroy(c->tm.t0);
         hipEventDestroy(c->tm.t1);
         hipEventDestroy(c->tm.t2);
         hipEventDestroy(c->desc_done);
         if (c->ws_done) hipEventDestroy(c->ws_done);
-        if (c->desc_pinned) hipHostFree(c->desc_pinned);
+        if (c->desc_pinned) hipHostFree(c->desc_pinned);  // teardown
         hipStreamDestroy(c->st);
     }
     delete c;
@@ -581,7 +566,8 @@ int lsmb_sync(lsmb_ctx* c) {
     if (!c) return fail(LSMB_EINVAL, "null ctx");
     DevGuard g(c->dev);
     HIP_TRY(hipStreamSynchronize(c->st));
-    return check_device_error(c);
+    report_stats(c);
+    return LSMB_OK;
 }
 
 int lsmb_build_fixed_dev(lsmb_ctx* c, const void* d_keys, uint32_t key_len, uint64_t n,
@@ -930,15 +916,28 @@ int fset_wait_probes(lsmb_fset* fs) {
     return LSMB_OK;
 }
 
-// After a probe on stream st: remember it so later rewrites wait for it.
+// After a probe on stream st: remember it so later rewrites wait for it.  At
+// most kFsetProbeStreams streams are tracked (a caller probing on pooled or
+// per-request streams would otherwise grow the list, and every add would wait
+// on all of it): a new stream past that takes the least recently used entry,
+// whose probe the host waits for first.
+constexpr size_t kFsetProbeStreams = 4;
+
 int fset_note_probe(lsmb_fset* fs, hipStream_t st) {
-    for (auto& pe : fs->probe_ev)
-        if (pe.first == st) {
-            HIP_TRY(hipEventRecord(pe.second, st));
+    for (size_t i = 0; i < fs->probe_ev.size(); i++)
+        if (fs->probe_ev[i].first == st) {
+            HIP_TRY(hipEventRecord(fs->probe_ev[i].second, st));
+            std::rotate(fs->probe_ev.begin() + i, fs->probe_ev.begin() + i + 1, fs->probe_ev.end());  // most recent last
             return LSMB_OK;
         }
     hipEvent_t ev;
-    HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    if (fs->probe_ev.size() < kFsetProbeStreams) {
+        HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    } else {
+        ev = fs->probe_ev.front().second;
+        HIP_TRY(hipEventSynchronize(ev));
+        fs->probe_ev.erase(fs->probe_ev.begin());
+    }
     fs->probe_ev.push_back({st, ev});
     HIP_TRY(hipEventRecord(ev, st));
     return LSMB_OK;
@@ -983,8 +982,8 @@ int fset_refresh(lsmb_fset* fs) {
         blob.insert(blob.end(), p.begin(), p.end());
     }
     if (int rc = fset_wait_probes(fs)) return rc;  // no probe may still read the old descriptors
-    // grow geometrically from 4 KiB: a re-allocation frees the old buffer, and
-    // hipFree waits for the whole device
+    // grow geometrically from 4 KiB (an outgrown buffer is retired, not freed:
+    // DevBuf)
     size_t want = 4096;
     while (want < blob.size()) want *= 2;
     HIP_TRY(fs->ranges.ensure(want));

@@ -111,16 +111,24 @@ __global__ __launch_bounds__(kCrcLanes) void k_crc32(const uint8_t* __restrict__
     uint64_t i = a;
     if (a < e) {
         // 4 bytes per step (slicing-by-4); the piece start is 512-B aligned
-        // from d, whose alignment the caller keeps at 4 B (else the byte loop)
-        if ((reinterpret_cast<uintptr_t>(d) & 3) == 0) {
+        // from d: 16-B loads where d is 16-B aligned, dword loads where it is
+        // only 4-B aligned (a uint4 access must be 16-B aligned), else the
+        // byte loop
+        auto step4 = [&](uint32_t w) {
+            const uint32_t x = c ^ w;
+            c = t[3][x & 0xFF] ^ t[2][(x >> 8) & 0xFF] ^ t[1][(x >> 16) & 0xFF] ^ t[0][x >> 24];
+        };
+        const uintptr_t al = reinterpret_cast<uintptr_t>(d);
+        if ((al & 15) == 0) {
             for (; i + 16 <= e; i += 16) {
                 const uint4 v = *reinterpret_cast<const uint4*>(d + i);
-                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const uint32_t x = c ^ w[q];
-                    c = t[3][x & 0xFF] ^ t[2][(x >> 8) & 0xFF] ^ t[1][(x >> 16) & 0xFF] ^ t[0][x >> 24];
-                }
+                step4(v.x), step4(v.y), step4(v.z), step4(v.w);
+            }
+        } else if ((al & 3) == 0) {
+            for (; i + 16 <= e; i += 16) {
+                const uint32_t* q = reinterpret_cast<const uint32_t*>(d + i);
+                const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];
+                step4(w0), step4(w1), step4(w2), step4(w3);
             }
         }
         for (; i < e; i++) c = t[0][(c ^ d[i]) & 0xFF] ^ (c >> 8);

@@ -4,6 +4,7 @@
 
 #include <stdint.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -13,22 +14,63 @@
 namespace lsmb {
 
 // A grow-only device buffer.
+//
+// Growing never frees: ROCm's hipFree (and hipHostFree) waits for every stream
+// of the device, so a free on the build path would stall every other context
+// (a flush next to a background compaction, src/compaction/scheduler.rs:37).
+// An outgrown buffer is retired instead — kernels queued on other streams may
+// still read it — and freed by release() at teardown (lsmb_close and the
+// handles' close functions, after their streams are synchronised).  Growth is
+// at least 1.5x, so the retired buffers never add up to more than twice the
+// live one.  Only when the device is out of memory are the retired buffers
+// freed early (a device-wide wait, but no failure).
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    std::vector<void*> retired;
     hipError_t ensure(size_t want) {
         if (want <= bytes) return hipSuccess;
-        if (p) hipFree(p);
-        p = nullptr;
-        bytes = 0;
-        hipError_t e = hipMalloc(&p, want);
-        if (e == hipSuccess) bytes = want;
-        return e;
+        size_t cap = std::max(want, bytes + bytes / 2);
+        void* q = nullptr;
+        hipError_t e = hipMalloc(&q, cap);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            cap = want;
+            e = hipMalloc(&q, cap);
+        }
+        if (e != hipSuccess && !retired.empty()) {  // out of memory: free what no longer grows
+            (void)hipGetLastError();
+            free_retired();
+            e = hipMalloc(&q, cap);
+        }
+        if (e != hipSuccess) return e;
+        if (p) retired.push_back(p);
+        p = q;
+        bytes = cap;
+        return hipSuccess;
+    }
+    void free_retired() {
+        for (void* r : retired) (void)hipFree(r);  // teardown / out-of-memory only
+        retired.clear();
     }
     void release() {
-        if (p) hipFree(p);
+        free_retired();
+        if (p) (void)hipFree(p);  // teardown
         p = nullptr;
         bytes = 0;
+    }
+};
+
+// Pinned host staging with the same policy (hipHostFree waits for the device
+// too): outgrown blocks are retired and freed at teardown.
+struct PinnedPool {
+    std::vector<void*> retired;
+    void retire(void* p) {
+        if (p) retired.push_back(p);
+    }
+    void release() {
+        for (void* r : retired) (void)hipHostFree(r);  // teardown
+        retired.clear();
     }
 };
 
@@ -79,8 +121,7 @@ struct lsmb_ctx {
     lsmb::DevBuf ws_regions, ws_counts;  // partition / tiled workspace
     lsmb::DevBuf crc_parts;              // CRC-32 workgroup partials (crc32.hip)
     lsmb::DevBuf ws_hashes;              // k_hash records (var-len / odd-length keys)
-    lsmb::DevBuf err;                    // device error flag of the partition kernels
-    uint32_t* err_host = nullptr;        // pinned mirror read at sync
+    lsmb::DevBuf err;                    // LSMB_STATS builds: pass A's overflow counters
     // The workspace above is shared by every build on this context, whatever
     // stream it is issued on: ws_done marks the last build that used it, and a
     // build on another stream waits for it first (build_dev).
@@ -104,7 +145,7 @@ struct lsmb_ctx {
     uint64_t offs_pin_cap[2] = {0, 0};
     uint8_t* pin_small = nullptr;  // pinned staging of small host builds (host_build_small)
     uint64_t pin_small_cap = 0;
-    bool ran_partition = false;    // a partition build ran since the last error-flag check
+    lsmb::PinnedPool pinned_retired;  // outgrown pinned staging, freed by lsmb_close
 };
 
 namespace lsmb {
@@ -125,9 +166,9 @@ int host_build_dev(lsmb_ctx* c, const uint8_t* data, const uint64_t* offsets, ui
 void host_insert_batch(const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
                        uint32_t num_bits, uint32_t k, uint64_t* words);
 
-// Reads (and clears) the kernels' device error flag.  Requires the work that
-// could set it to have completed.
-int check_device_error(lsmb_ctx* c);
+// LSMB_STATS builds only: prints and clears pass A's overflow counters
+// (ring overflow, full regions).  Requires the builds to have completed.
+void report_stats(lsmb_ctx* c);
 // CRC-32 (crc32fast::hash / zlib crc32) of device bytes appended to `crc`
 // (crc32.hip); synchronises `st`.
 int crc32_dev(lsmb_ctx* c, const uint8_t* d, uint64_t len, uint32_t crc, hipStream_t st, uint32_t* out);

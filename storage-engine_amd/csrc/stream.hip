@@ -52,6 +52,7 @@ struct lsmb_stream {
     uint64_t total = 0;           // keys added since open / reset
     bool on_device = false;       // a chunk was submitted (the words live on the device)
     int failed = 0;               // sticky error code of an add
+    PinnedPool retired;           // outgrown pinned staging (hipHostFree waits for the device)
 };
 
 namespace {
@@ -63,22 +64,24 @@ void* host_alloc(bool pinned, uint64_t bytes) {
     if (pinned) return hipHostMalloc(&p, bytes, 0) == hipSuccess ? p : nullptr;
     return malloc(bytes);
 }
-void host_free(bool pinned, void* p) {
+// Outgrown staging: pinned blocks are retired until close (a free would wait
+// for every stream of the device), heap blocks freed.
+void host_retire(lsmb_stream* st, bool pinned, void* p) {
     if (!p) return;
     if (pinned)
-        (void)hipHostFree(p);
+        st->retired.retire(p);
     else
         free(p);
 }
 
-int slot_reserve(lsmb_stream::Slot& s, bool pinned, uint64_t want_bytes, uint64_t want_keys) {
+int slot_reserve(lsmb_stream* st, lsmb_stream::Slot& s, bool pinned, uint64_t want_bytes, uint64_t want_keys) {
     if (want_bytes > s.data_cap) {
         uint64_t cap = std::max<uint64_t>(kStreamMinBytes, s.data_cap * 2);
         while (cap < want_bytes) cap *= 2;
         uint8_t* p = (uint8_t*)host_alloc(pinned, cap);
         if (!p) return fail(LSMB_ENOMEM, "stream: key staging (%llu B)", (unsigned long long)cap);
         if (s.bytes) memcpy(p, s.data, s.bytes);
-        host_free(pinned, s.data);
+        host_retire(st, pinned, s.data);
         s.data = p;
         s.data_cap = cap;
     }
@@ -91,7 +94,7 @@ int slot_reserve(lsmb_stream::Slot& s, bool pinned, uint64_t want_bytes, uint64_
             memcpy(p, s.offs, (s.nkeys + 1) * 8);
         else
             p[0] = 0;
-        host_free(pinned, s.offs);
+        host_retire(st, pinned, s.offs);
         s.offs = p;
         s.keys_cap = cap;
     }
@@ -139,7 +142,7 @@ int stream_add(lsmb_stream* st, const uint8_t* key, uint64_t len) {
         s = &st->slot[st->cur];
     }
     if (s->bytes + len > s->data_cap || s->nkeys + 2 > s->keys_cap)
-        if (int rc = slot_reserve(*s, st->c != nullptr, s->bytes + len, s->nkeys + 1)) return rc;
+        if (int rc = slot_reserve(st, *s, st->c != nullptr, s->bytes + len, s->nkeys + 1)) return rc;
     if (len) memcpy(s->data + s->bytes, key, len);
     s->bytes += len;
     s->offs[++s->nkeys] = s->bytes;
@@ -186,9 +189,8 @@ int stream_finish(lsmb_stream* st, uint8_t* out) {
     }
     HIP_TRY(hipMemcpyAsync(out, st->words.p, st->nw * 8, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(hipStreamSynchronize(c->st));
-    const int rc = check_device_error(c);
     stream_rewind(st);
-    return rc;
+    return LSMB_OK;
 }
 
 }  // namespace
@@ -215,7 +217,7 @@ int lsmb_stream_open(lsmb_ctx* c, uint32_t num_bits, uint32_t num_hashes, lsmb_s
             }
     }
     for (auto& s : st->slot)
-        if (int rc = slot_reserve(s, c != nullptr, kStreamMinBytes, kStreamMinBytes / 16)) {
+        if (int rc = slot_reserve(st, s, c != nullptr, kStreamMinBytes, kStreamMinBytes / 16)) {
             lsmb_stream_close(st);
             return rc;
         }
@@ -292,9 +294,10 @@ void lsmb_stream_close(lsmb_stream* st) {
         st->words.release();
     }
     for (auto& s : st->slot) {
-        host_free(pinned, s.data);
-        host_free(pinned, s.offs);
+        host_retire(st, pinned, s.data);
+        host_retire(st, pinned, s.offs);
     }
+    st->retired.release();
     delete st;
 }
 

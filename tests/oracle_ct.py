@@ -28,6 +28,33 @@ def load():
     path = os.path.join(ODIR, "liboracle.so")
     if not os.path.exists(path):
         build()
+    _lib = _bind(path)
+    return _lib
+
+
+NATIVE_FLAGS = ["-O3", "-march=native", "-fPIC", "-std=c11", "-D_GNU_SOURCE"]
+
+
+def load_native(outdir=None):
+    """The oracle compiled on THIS host with -O3 -march=native (BASELINE.md's
+    CPU-baseline flags): bench.py's cpu_baseline leg builds it on the GPU box,
+    whose CPU differs from the build container's.  Returns (Oracle, how);
+    falls back to the portable liboracle.so when no C compiler is present."""
+    import shutil
+    import tempfile
+    cc = shutil.which(os.environ.get("CC", "gcc")) or shutil.which("cc")
+    if cc:
+        d = outdir or tempfile.mkdtemp(prefix="lsmb_oracle_")
+        out = os.path.join(d, "liboracle_native.so")
+        r = subprocess.run([cc] + NATIVE_FLAGS + ["-shared", "-o", out, os.path.join(ODIR, "bloom_oracle.c"),
+                                                  "-lm", "-lpthread"], capture_output=True, text=True)
+        if r.returncode == 0:
+            return _bind(out), "oracle/bloom_oracle.c, %s %s (built on this host)" % (os.path.basename(cc),
+                                                                                        " ".join(NATIVE_FLAGS[:2]))
+    return load(), "oracle/liboracle.so (portable -O3; no C compiler for a -march=native build)"
+
+
+def _bind(path):
     lib = ctypes.CDLL(path)
     V, I, Z, D = None, ctypes.c_int, ctypes.c_size_t, ctypes.c_double
     U32, U64 = ctypes.c_uint32, ctypes.c_uint64
@@ -50,8 +77,7 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    _lib = Oracle(lib)
-    return _lib
+    return Oracle(lib)
 
 
 def _p(a, t):

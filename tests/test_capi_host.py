@@ -175,6 +175,28 @@ def test_no_device_wide_synchronisation_in_library():
         assert not re.search(r"\bhipMemset\s*\(", code), path
 
 
+def test_no_free_on_the_build_path():
+    """ROCm's hipFree / hipHostFree wait for every stream
+    of the device, so a buffer that grows mid-run must not be freed (DevBuf and
+    PinnedPool retire it until teardown).  Every free in the library sits in a
+    teardown path, marked `// teardown` on its line, and the growth paths
+    (DevBuf::ensure, the pinned staging of host builds and streams) retire."""
+    import glob
+    srcs = glob.glob(os.path.join(ROOT, "storage-engine_amd", "csrc", "*.hip")) + \
+        glob.glob(os.path.join(ROOT, "storage-engine_amd", "csrc", "*.hpp"))
+    n = 0
+    for path in srcs:
+        for no, line in enumerate(open(path), 1):
+            code = line.split("//", 1)[0]
+            if re.search(r"\bhip(Host)?Free(Async)?\s*\(", code):
+                n += 1
+                assert "// teardown" in line, "%s:%d frees outside a teardown path: %s" % (path, no, line.strip())
+    assert n > 0
+    ctx = open(os.path.join(ROOT, "storage-engine_amd", "csrc", "ctx.hpp")).read()
+    ensure = ctx[ctx.index("hipError_t ensure(size_t want)"):ctx.index("void free_retired()")]
+    assert "retired.push_back(p)" in ensure and "hipFree" not in ensure.replace("free_retired()", "")
+
+
 def test_sweep_ranges_tile_the_filter():
     """lsmb_build_sweeps / lsmb_sweep_words (host-only planning): the sweeps'
     word ranges are contiguous, disjoint and cover the filter; C5's 2^32-1-bit

@@ -39,6 +39,7 @@ def test_build_block_crc_host_path():
 
 @pytest.mark.gpu
 def test_crc32_dev_lengths_and_alignment():
+    # offsets 4, 8, 12: 4-B aligned (dword loads); 0, 16: 16-B loads; odd: byte loop
     import torch
     ctx = lsmbloom.Context(0)
     dev = torch.device("cuda:0")
@@ -47,7 +48,8 @@ def test_crc32_dev_lengths_and_alignment():
     d = torch.from_numpy(host).to(dev)
     kb = 128 * 1024
     for off, n in [(0, 0), (0, 1), (0, 511), (0, 512), (0, 513), (0, kb - 1), (0, kb), (0, kb + 1),
-                   (0, 3 * kb + 4099), (1, 1000), (3, kb + 5), (4, 2 * kb), (0, host.size), (5, host.size - 5)]:
+                   (0, 3 * kb + 4099), (1, 1000), (3, kb + 5), (4, 2 * kb), (8, kb + 7), (12, 3 * kb + 1),
+                   (16, kb), (0, host.size), (5, host.size - 5)]:
         got = ctx.crc32_dev(d[off:off + n], n)
         assert got == zlib.crc32(host[off:off + n].tobytes()), (off, n)
     # appended to a prefix CRC

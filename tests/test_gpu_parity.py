@@ -494,3 +494,53 @@ def test_c4_full_size_properties(ctx, oracle):
         assert f.may_contain(key)
     del data, offs, mono
     torch.cuda.empty_cache()
+
+
+# ---------------------------------------------------------------- C3 at full size
+def test_c3_full_size_every_answer(ctx, oracle):
+    """C3 (10 M lookups x 8 SST filters, configs[2]) with
+    every answer byte compared, not a sample: the plain batched probe
+    (may_contain per table, src/sstable/reader.rs:197) and the filter-set form
+    with SSTable::get's range pre-check (reader.rs:192-199, shape of
+    tests/bloom_sstable_integration_tests.rs:66-113), same-size and mixed-size
+    tables, against the oracle (tests/c3_ref.py: bench.py's workload)."""
+    import torch
+    import c3_ref
+    Q, F = 10_000_000, 8
+    mask, fset_ref, mixed_ref = c3_ref.answers(oracle, Q, F, threads=16)
+    members, q_host, _ = c3_ref.workload(oracle, Q, F)
+    dev = torch.device("cuda:0")
+    nb, k = lsmbloom.params(1000, 0.01)
+    mem = torch.from_numpy(members).to(dev)
+    filt = []
+    for f in range(F):
+        w = torch.zeros(lsmbloom.num_words(nb), dtype=torch.int64, device=dev)
+        ctx.build_fixed_dev(mem[f * 1000:(f + 1) * 1000], 16, 1000, nb, k, w)
+        filt.append((w, nb, k))
+    q = torch.from_numpy(q_host).to(dev)
+    out = torch.zeros((Q, 1), dtype=torch.uint8, device=dev)
+    ctx.probe_dev(filt, q, Q, out, key_len=16)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    bad = np.flatnonzero(got[:, 0] != mask[:, 0])
+    assert bad.size == 0, "probe answers differ at %d rows, first %s" % (bad.size, bad[:5])
+    fout = torch.zeros(Q, dtype=torch.int64, device=dev)
+    for mixed in (False, True):
+        fs = lsmbloom.FilterSet(ctx)
+        nb4, k4 = lsmbloom.params(4000, 0.01)
+        for f in range(F):
+            if mixed and f >= F // 2:
+                rows = oracle.key16(0xF100 + f, 0, 4000)
+                bf = lsmbloom.BloomFilter(oracle.build_fixed(rows, 16, nb4, k4), k4, nb4)
+            else:
+                rows = members[f * 1000:(f + 1) * 1000]
+                bf = lsmbloom.BloomFilter(filt[f][0].cpu().numpy().view(np.uint64), k, nb)
+            lo, hi = c3_ref.sorted_bounds(rows)
+            assert fs.add_filter(bf, lo.tobytes(), hi.tobytes()) == f
+        fs.probe_dev(q, Q, fout, key_len=16)
+        torch.cuda.synchronize()
+        ref = mixed_ref if mixed else fset_ref
+        g = fout.cpu().numpy().view(np.uint64)
+        bad = np.flatnonzero(g != ref)
+        assert bad.size == 0, "filter-set (mixed=%s) answers differ at %d rows" % (mixed, bad.size)
+        fs.close()
