@@ -103,6 +103,19 @@ def test_fset_fixed_len_keys_and_device_probe(oracle):
     fs.probe_dev(dq, q.shape[0], dout, key_len=16)
     torch.cuda.synchronize()
     assert np.array_equal(dout.cpu().numpy().view(np.uint64), got)
+    # probes on many streams (per-request / pooled streams): the set
+    # tracks at most 4 and waits for the evicted one; adds and removes between
+    # them still see every answer right
+    streams = [torch.cuda.Stream("cuda:0") for _ in range(9)]
+    outs = [torch.zeros_like(dout) for _ in streams]
+    for rep in range(3):
+        for st, o in zip(streams, outs):
+            fs.probe_dev(dq, q.shape[0], o, key_len=16, stream=st.cuda_stream)
+        extra = fs.add_filter(BloomFilter(tables[0][0], tables[0][2], tables[0][1]), b"", b"")  # empty-range table
+        fs.remove(extra)
+    torch.cuda.synchronize()
+    for o in outs:
+        assert np.array_equal(o.cpu().numpy().view(np.uint64), got)
     # unaligned fixed-length keys (FixedN path)
     q7 = np.ascontiguousarray(q[:5000, :7])
     got7 = fs.probe(q7, key_len=7)

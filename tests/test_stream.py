@@ -69,14 +69,23 @@ def test_stream_batches_many_chunks(ctx, oracle, small_chunks, filter_n):
 
 
 def test_stream_reuse_reset_and_threshold(ctx, oracle):
+    # The gpu marker's fixture forces host_max_keys() = 0; a ctx-backed stream
+    # must also cross a real threshold: at 64 keys the run finishes with the
+    # host loop out of the pinned staging, at 65 it goes to the device
+    # (ADVICE r02).
     nb, k = lsmbloom.params(50_000, 0.01)
     st = lsmbloom.KeyStream(ctx, nb, k)
-    for rnd, n in enumerate((50_000, 100, lsmbloom.host_max_keys(), lsmbloom.host_max_keys() + 1, 0)):
-        keys = keygen.key16(0x1000 + rnd, 0, n) if n else np.zeros((0, 16), np.uint8)
-        for i in range(n):
-            st.add(bytes(keys[i]))
-        w = st.finish_words()
-        assert np.array_equal(w, oracle.build_fixed(keys, 16, nb, k)), (rnd, n)
+    old = lsmbloom.host_max_keys()
+    lsmbloom.set_host_max_keys(64)
+    try:
+        for rnd, n in enumerate((50_000, 100, 64, 65, 1, 0, 64)):
+            keys = keygen.key16(0x1000 + rnd, 0, n) if n else np.zeros((0, 16), np.uint8)
+            for i in range(n):
+                st.add(bytes(keys[i]))
+            w = st.finish_words()
+            assert np.array_equal(w, oracle.build_fixed(keys, 16, nb, k)), (rnd, n)
+    finally:
+        lsmbloom.set_host_max_keys(old)
     nb2, k2 = lsmbloom.params(2_000_000, 0.001)
     st.reset(nb2, k2)
     keys = keygen.key16(7, 0, 300_000)

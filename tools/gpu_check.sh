@@ -8,9 +8,9 @@ K=${2:-}
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 if [ -n "$K" ]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$K" > gpurun_out/${TAG}_tests.log 2>&1
+  timeout -k 10 600 python -u -m pytest tests -m gpu --maxfail=3 -v --timeout 300 --timeout-method thread -k "$K" > gpurun_out/${TAG}_tests.log 2>&1
 else
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1
+  timeout -k 10 600 python -u -m pytest tests -m gpu --maxfail=3 -v --timeout 300 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1
 fi
 rc=$?
 echo "tests rc=$rc"
