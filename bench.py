@@ -487,6 +487,8 @@ def main():
         out["roofline"]["traffic_source"] = tr["source"]
         if tr["fresh"]:
             out["roofline"]["traffic"] = tr["bytes"]
+            if tr.get("valu_insts"):
+                out["roofline"]["secondary"] = valu_roofline(tr, out["roofline"]["kernel_ms"], npg)
         else:
             out["roofline"]["traffic_stale"] = "kernel sources changed since %s was profiled" % tr["source"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -768,7 +770,34 @@ def committed_traffic():
         return None
     t = json.load(open(p))
     return {"bytes": t.get("build_bytes"), "source": "%s (%s)" % (os.path.relpath(p, ROOT), t.get("profile")),
-            "fresh": t.get("kernel_src_sha") == build_sources_sha()}
+            "fresh": t.get("kernel_src_sha") == build_sources_sha(), "valu_insts": t.get("build_valu_insts")}
+
+
+# VALU issue ceiling: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2
+# cycles per SIMD (SIMD-32), 2.4 GHz (MI355X_MICROARCH.md: execution model).
+VALU_PEAK_WAVE_INSTS = 256 * 4 * 2.4e9 / 2
+# XXH3-128 of 16-B keys + the 7 exact positions alone (no binning, no filter
+# traffic), 100 M keys at full occupancy: tools/mb_hash.hip.
+HASH_WALK_FLOOR_MS_PER_1E8 = 0.47
+
+
+def valu_roofline(tr, kernel_ms, n):
+    """roofline.secondary: the build's VALU work against the VALU issue
+    ceiling, from the committed PMC profile's SQ_INSTS_VALU (whole-chip wave64
+    VALU instructions per build).  Quarter-rate instructions (the 64-bit
+    multiplies of XXH3 and of the exact reductions) take longer than the 2
+    cycles counted here, so the true ceiling is lower: frac is a lower bound
+    on how busy the VALU is."""
+    insts = tr["valu_insts"]
+    achieved = insts / (kernel_ms * 1e-3)
+    return {"bound": "valu", "achieved": round(achieved / 1e12, 4), "peak": round(VALU_PEAK_WAVE_INSTS / 1e12, 4),
+            "unit": "T wave64-VALU-inst/s", "frac": round(achieved / VALU_PEAK_WAVE_INSTS, 4),
+            "valu_insts_per_build": insts, "valu_insts_per_wave_key": round(insts * 64 / n, 1),
+            "valu_issue_floor_ms": round(insts / VALU_PEAK_WAVE_INSTS * 1e3, 4),
+            "hash_walk_floor_ms": round(HASH_WALK_FLOOR_MS_PER_1E8 * n / 1e8, 4),
+            "hash_walk_floor_frac_of_hbm_roofline": round(
+                (16 * n + 8 * ((956715292 + 63) // 64)) / (HASH_WALK_FLOOR_MS_PER_1E8 * n / 1e8 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "source": tr["source"]}
 
 
 def fixture_check(words, name, num_bits):

@@ -42,18 +42,37 @@
 #ifndef LSMB_ABL
 #define LSMB_ABL 0
 #endif
-#ifndef LSMB_PIPE
-#define LSMB_PIPE 0
-#endif
 #ifndef LSMB_STORE_AUX
 #define LSMB_STORE_AUX 0  // pass A region stores' cache policy bits (measurement variants)
 #endif
 #ifndef LSMB_APPLY_U
 #define LSMB_APPLY_U 8  // pass B: 16-B region loads in flight per lane
 #endif
+// LSMB_STAMP=1 (diagnostic build for tools/, never the product): pass A's
+// phase sections timed with s_memtime, summed per wave in scalar registers
+// and added into g_stamp once per wave (MI355X stamp idiom): claims + hash +
+// slot writes | barrier 1 wait | flush | barrier 2 wait.  Read its shares,
+// not its length.
+#ifndef LSMB_STAMP
+#define LSMB_STAMP 0
+#endif
+#ifndef LSMB_WALKFIRST
+#define LSMB_WALKFIRST 0  // measurement variant: the walk pinned between the fill read and its use
+#endif
 
 namespace lsmb {
 namespace {
+
+#if LSMB_STAMP
+__device__ unsigned long long g_stamp[8];
+__device__ __forceinline__ uint64_t stamp() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#endif
 
 using ks::Fixed16;
 using ks::FixedN;
@@ -251,8 +270,8 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
     // Local positions (p - b0 * 2^20) of the key this lane claims in the
     // current phase; `sink` where there is none.  kinc: this key's increment.
     uint32_t pos[NP], kinc[PER];
-    auto walk_positions = [&](const H128& h, bool ok, uint32_t* out) {
-        W walk(md, h.lo, h.hi);
+    auto walk_positions = [&](const typename Src::Seed& h, bool ok, uint32_t* out) {
+        W walk(md, h);
 #pragma unroll
         for (int q = 0; q < KMAX; q++) {
             if (EXACT || (uint32_t)q < k) {
@@ -281,43 +300,31 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
     // register copy forces a vmcnt drain).  gfx9 retires loads and stores in
     // one in-order vmcnt queue: a key load completes only after every older
     // region store, so the distance must cover the store round trip too.
-    // LSMB_PIPE=1 (measurement variant): a key goes through three phases —
-    // hashed in phase it-2, walked in phase it-1, claimed in phase it — so
-    // every phase runs two independent dependency chains per lane.  Measured
-    // slower (pass A 1.05 -> 1.10 ms at C2); the
-    // default hashes and walks key it+1 in one chain during phase it.
-    constexpr bool kPipe = LSMB_PIPE != 0;
     Pre pb0[PER], pb1[PER], pb2[PER], pb3[PER];  // phase m's keys live in pb[m % 4]
-    bool nok[PER];
-    H128 nh[PER];  // kPipe: key it+1's hash
 #pragma unroll
     for (int j = 0; j < PER; j++) {
         const bool ok = key_ok(0, j);
         const Pre p = src.fetch(key_index(0) + j, ok);
-        const H128 h = ok ? src.hash_pre(p, key_index(0) + j) : H128{0, 0};
+        const typename Src::Seed h = ok ? src.hash_pre(p, key_index(0) + j) : typename Src::Seed{};
         walk_positions(h, ok, pos + j * KMAX);
         kinc[j] = ok ? kInc : 0u;
-        if constexpr (kPipe) {
-            nok[j] = key_ok(1, j);
-            const Pre p1 = src.fetch(key_index(1) + j, nok[j]);
-            nh[j] = nok[j] ? src.hash_pre(p1, key_index(1) + j) : H128{0, 0};
-        }
     }
-    if constexpr (kPipe) {
-        fetch_keys(2, pb2);
-        fetch_keys(3, pb3);
-        fetch_keys(4, pb0);
-        fetch_keys(5, pb1);
-    } else {
-        fetch_keys(1, pb1);
-        fetch_keys(2, pb2);
-        fetch_keys(3, pb3);
-        fetch_keys(4, pb0);
-    }
+    fetch_keys(1, pb1);
+    fetch_keys(2, pb2);
+    fetch_keys(3, pb3);
+    fetch_keys(4, pb0);
     __syncthreads();
 
-    // One phase: claim key it's positions, hash and walk key it+1 (from
-    // `pre`) and reload `pre` with key it+1+kAhead, store the entries, flush.
+#if LSMB_STAMP
+    uint64_t st_sum[4] = {0, 0, 0, 0}, st_prev = stamp(), st_t;
+#endif
+    // One phase: claim key it's positions; hash key it+1 (from `pre`) and
+    // reload `pre` with key it+1+kAhead while the claims are in flight; store
+    // the entries; barrier; flush, with key it+1's position walk computed
+    // beside it; barrier.  The phase's VALU work is split over both barrier
+    // sections so neither is all-LDS (the claims, slot writes and flush) or
+    // all-VALU: stamps of the earlier form (hash and walk both before the
+    // first barrier) showed the flush section VALU-idle for ~29 % of a phase.
     auto phase = [&](uint64_t it, Pre (&pre)[PER]) __attribute__((always_inline)) {
         // Claims for this phase's keys, back to back.
         uint32_t got[NP];
@@ -335,37 +342,19 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
                 }
             }
         }
-        // While the claims are in flight: hash and walk key it+1, pinned here
-        // (an empty asm that consumes the positions): otherwise the compiler
-        // sinks the whole hash + walk below the barrier, where every wave
-        // computes while none has LDS work, and the claims' round trip is
-        // exposed instead.
-        uint32_t npos[NP], nkinc[PER];
-        bool nok2[PER];
-        H128 nh2[PER];
+        // While the claims are in flight: XXH3 of key it+1, pinned here (an
+        // empty asm consuming it), else the compiler sinks it past the
+        // barrier, where the claims' round trip is then exposed.
+        typename Src::Seed nh[PER];
+        bool nok[PER];
 #pragma unroll
         for (int j = 0; j < PER; j++) {
-            if constexpr (kPipe) {
-                walk_positions(nh[j], nok[j], npos + j * KMAX);
-                nkinc[j] = nok[j] ? kInc : 0u;
-                nok2[j] = key_ok(it + 2, j);
-                nh2[j] = src.hash_pre(pre[j], key_index(it + 2) + j);
-            } else {
-                const bool ok = key_ok(it + 1, j);
-                walk_positions(src.hash_pre(pre[j], key_index(it + 1) + j), ok, npos + j * KMAX);
-                nkinc[j] = ok ? kInc : 0u;
-            }
+            nok[j] = key_ok(it + 1, j);
+            nh[j] = src.hash_pre(pre[j], key_index(it + 1) + j);
         }
-        fetch_keys(it + (kPipe ? 2 : 1) + kAhead, pre);
+        fetch_keys(it + 1 + kAhead, pre);
 #pragma unroll
-        for (int q = 0; q < NP; q++)
-            if (EXACT || (uint32_t)q < k) asm volatile("" ::"v"(npos[q]));
-        if constexpr (kPipe) {
-#pragma unroll
-            for (int j = 0; j < PER; j++)
-                asm volatile("" ::"v"((uint32_t)nh2[j].lo), "v"((uint32_t)(nh2[j].lo >> 32)), "v"((uint32_t)nh2[j].hi),
-                             "v"((uint32_t)(nh2[j].hi >> 32)));
-        }
+        for (int j = 0; j < PER; j++) pin_seed(nh[j]);
         // Store the claimed entries.  Fast path (every claim of the wave fits
         // its ring): slot address = b * R4 + wrapped ring offset, one full-rate
         // 24-bit multiply-add, no per-position select.  A wave with an
@@ -405,17 +394,13 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
                 }
             }
         }
-#pragma unroll
-        for (int q = 0; q < NP; q++) pos[q] = npos[q];
-#pragma unroll
-        for (int j = 0; j < PER; j++) {
-            kinc[j] = nkinc[j];
-            if constexpr (kPipe) {
-                nok[j] = nok2[j];
-                nh[j] = nh2[j];
-            }
-        }
+#if LSMB_STAMP
+        st_t = stamp(), st_sum[0] += st_t - st_prev, st_prev = st_t;
+#endif
         lds_barrier();
+#if LSMB_STAMP
+        st_t = stamp(), st_sum[1] += st_t - st_prev, st_prev = st_t;
+#endif
 
         // Flush, wave-cooperative: every owner lane whose slice holds a full
         // 24-entry segment posts it as a job {group addresses, region offset}
@@ -426,16 +411,28 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
         // so the flush issues exactly kCoopRounds stores per wave per phase,
         // at a dropped offset where a lane has nothing to write — a static
         // store count also keeps the compiler's vmcnt waits for the
-        // prefetched keys exact.  A second segment of the same slice, or a
-        // region already full, takes the per-lane path below (rare).
-        uint32_t cnt = 0;
-        if (owner) {
-            cnt = min(fill[own] >> 16, R);
-            if (LSMB_ABL & 1) {
-                fill[own] = start;
-                cnt = 0;
-            }
+        // prefetched keys exact.  The common case is branch-free (every lane
+        // reads a fill word — non-owners the sink's — and writes a job entry,
+        // the non-posting ones into the table's last, scratch entry), so the
+        // walk below can fill the flush's LDS round trips; a second segment
+        // of the same slice, or a full region, takes the per-lane path (rare).
+        const uint32_t ownc = owner ? own : nb;  // non-owners: the sink's fill word (stays 0)
+        uint32_t fv = fill[ownc];
+#if LSMB_WALKFIRST
+        // Key it+1's positions (VALU only) while the fill word is read.
+        uint32_t npos[NP], nkinc[PER];
+#pragma unroll
+        for (int j = 0; j < PER; j++) {
+            walk_positions(nh[j], nok[j], npos + j * KMAX);
+            nkinc[j] = nok[j] ? kInc : 0u;
         }
+#pragma unroll
+        for (int q = 0; q < NP; q++)
+            if (EXACT || (uint32_t)q < k) asm volatile("" ::"v"(npos[q]));
+        asm volatile("" : "+v"(fv));
+#endif
+        uint32_t cnt = owner ? min(fv >> 16, R) : 0u;
+        if (LSMB_ABL & 1) cnt = 0;
         const bool has = cnt >= (uint32_t)kSegEntries;
         const char* ring = (const char*)sm + own * R4;
         uint4 x0, x1, y0, y1, z0, z1;
@@ -470,45 +467,55 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
 #endif
         };
         // 1. post jobs (owner lanes with a full segment and room in the region)
+        constexpr uint32_t kPost = kBinJobsPerWave - 1;  // the last entry is scratch
         const bool coop = has && segs < a.cap;
         const uint64_t cm = __ballot(coop);
-        const uint32_t jobs = min((uint32_t)__popcll(cm), kBinJobsPerWave);  // wave-uniform
-        bool posted = false;
-        if (coop) {
-            const uint32_t j = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
-            if (j < kBinJobsPerWave) {
-                const uint32_t rb = own * R4;
-                uint32_t g1 = start + 32, g2 = start + 64;
-                g1 = min(g1, g1 - R4);
-                g2 = min(g2, g2 - R4);
-                jobtab[wave * kBinJobsPerWave + j] =
-                    make_uint4(rb + start, rb + g1, rb + g2, ((a.b0 + own) * a.cap + segs) * 64u);
-                posted = true;
-            }
+        const uint32_t jobs = min((uint32_t)__popcll(cm), kPost);  // wave-uniform
+        const uint32_t jr = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
+        const bool posted = coop && jr < kPost;
+        {
+            const uint32_t rb = ownc * R4;
+            uint32_t g1 = start + 32, g2 = start + 64;
+            g1 = min(g1, g1 - R4);
+            g2 = min(g2, g2 - R4);
+            jobtab[wave * kBinJobsPerWave + (posted ? jr : kPost)] =
+                make_uint4(rb + start, rb + g1, rb + g2, ((a.b0 + own) * a.cap + segs) * 64u);
         }
-        // (the job table is this wave's own: its LDS writes and reads stay in order)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#if !LSMB_WALKFIRST
+        // Key it+1's positions (VALU only), beside the flush's LDS round trips.
+        uint32_t npos[NP], nkinc[PER];
+#pragma unroll
+        for (int j = 0; j < PER; j++) {
+            walk_positions(nh[j], nok[j], npos + j * KMAX);
+            nkinc[j] = nok[j] ? kInc : 0u;
+        }
+#endif
         // 2. kCoopRounds store instructions: lane L writes 16 B of job r*16 + L/4
-        constexpr uint32_t kCoopRounds = (kBinJobsPerWave + 15) / 16;
+        constexpr uint32_t kCoopRounds = (kPost + 15) / 16;
 #pragma unroll
         for (uint32_t r = 0; r < kCoopRounds; r++) {
             const uint32_t j = r * 16 + (lane >> 2), l = lane & 3;
-            uint32_t off = kDrop;
-            uint2 w0 = make_uint2(0, 0), w1 = make_uint2(0, 0);
-            if (j < jobs) {
-                const uint4 jb = jobtab[wave * kBinJobsPerWave + j];
-                // segment word 2l+e = pack3<SL>(group0[2l+e], group1[2l+e], group2[2l+e])
-                const uint2 a0 = *(const uint2*)((const char*)sm + jb.x + 8 * l);
-                const uint2 a1 = *(const uint2*)((const char*)sm + jb.y + 8 * l);
-                const uint2 a2 = *(const uint2*)((const char*)sm + jb.z + 8 * l);
-                w0 = pack3w<SL>(a0.x, a1.x, a2.x);
-                w1 = pack3w<SL>(a0.y, a1.y, a2.y);
-                off = (LSMB_ABL & 16) ? kDrop : jb.w + 16 * l;
-            }
+            const bool valid = j < jobs;
+            const uint4 jb = jobtab[wave * kBinJobsPerWave + (valid ? j : kPost)];
+            // segment word 2l+e = pack3<SL>(group0[2l+e], group1[2l+e], group2[2l+e])
+            const uint2 a0 = *(const uint2*)((const char*)sm + jb.x + 8 * l);
+            const uint2 a1 = *(const uint2*)((const char*)sm + jb.y + 8 * l);
+            const uint2 a2 = *(const uint2*)((const char*)sm + jb.z + 8 * l);
+            const uint2 w0 = pack3w<SL>(a0.x, a1.x, a2.x), w1 = pack3w<SL>(a0.y, a1.y, a2.y);
+            const uint32_t off = (valid && !(LSMB_ABL & 16)) ? jb.w + 16 * l : kDrop;
             if (!(LSMB_ABL & 8)) __builtin_amdgcn_raw_buffer_store_b128(u32x4{w0.x, w0.y, w1.x, w1.y}, rgn, off, 0, LSMB_STORE_AUX);
         }
-        // 3. owners advance past the posted segment; the rest per lane
-        if (has) {
+        // 3. owners advance past the posted segment; the rest per lane (rare)
+        const bool rare = has && (!posted || cnt >= 2u * kSegEntries);
+        if (__builtin_expect(__ballot(rare) == 0, 1)) {
+            uint32_t s2 = start + 96;
+            s2 = min(s2, s2 - R4);
+            const uint32_t rem = cnt - (uint32_t)kSegEntries;
+            const uint32_t nf = has ? ((s2 + 4 * rem) | (rem << 16)) : ((LSMB_ABL & 1) && owner ? start : fv);
+            start = has ? s2 : start;
+            segs = has ? segs + 1 : segs;
+            fill[ownc] = nf;  // unchanged where nothing was flushed (non-owners: the sink's 0)
+        } else if (has) {
             if (!posted) {
                 read_segment();
                 if (segs < a.cap)
@@ -533,27 +540,42 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
             }
             const uint32_t rem = cnt - nf * (uint32_t)kSegEntries;
             fill[own] = (start + 4 * rem) | (rem << 16);
+        } else if ((LSMB_ABL & 1) && owner) {
+            fill[own] = start;
         }
+#pragma unroll
+        for (int q = 0; q < NP; q++) {
+            if (EXACT || (uint32_t)q < k) asm volatile("" ::"v"(npos[q]));
+            pos[q] = npos[q];
+        }
+#pragma unroll
+        for (int j = 0; j < PER; j++) kinc[j] = nkinc[j];
+#if LSMB_STAMP
+        st_t = stamp(), st_sum[2] += st_t - st_prev, st_prev = st_t;
+#endif
         lds_barrier();
+#if LSMB_STAMP
+        st_t = stamp(), st_sum[3] += st_t - st_prev, st_prev = st_t;
+#endif
     };
     // Whole groups of kAhead phases (the last group's extra phases carry no
     // keys): no early exit, so the buffers keep their registers.
     const uint64_t groups = (iters + kAhead - 1) / kAhead;
     for (uint64_t g = 0; g < groups; g++) {
         const uint64_t it = g * kAhead;
-        if constexpr (kPipe) {
-            phase(it, pb2);
-            phase(it + 1, pb3);
-            phase(it + 2, pb0);
-            phase(it + 3, pb1);
-        } else {
-            phase(it, pb1);
-            phase(it + 1, pb2);
-            phase(it + 2, pb3);
-            phase(it + 3, pb0);
-        }
+        phase(it, pb1);
+        phase(it + 1, pb2);
+        phase(it + 2, pb3);
+        phase(it + 3, pb0);
     }
 
+#if LSMB_STAMP
+    if (lane == 0) {
+        for (int q = 0; q < 4; q++) atomicAdd(&g_stamp[q], (unsigned long long)st_sum[q]);
+        atomicAdd(&g_stamp[4], (unsigned long long)groups * kAhead);
+        atomicAdd(&g_stamp[5], 1ull);
+    }
+#endif
     // Segments still queued, then the last open segment (< 24 entries, padded
     // with copies of its first offset: setting a bit twice is a no-op), then
     // the region's segment count.  Rare tail work, one lane per slice.
@@ -581,6 +603,335 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
             cnt -= m;
         }
         a.counts[(uint64_t)(a.b0 + own) * a.grid + w] = segs;
+    }
+}
+
+// Pass A with specialised waves (k_bin2, k = KMAX exact).  The stamps of
+// k_bin (LSMB_STAMP) put a C2 phase at ~5 900 cycles: the claims and slot
+// writes of 16 waves (LDS-bound, ~2 100 LDS cycles of random-address atomics
+// and stores) with the hash beside them, then a flush that is a chain of
+// dependent LDS round trips (owner fill read -> job post -> job read ->
+// segment reads -> stores) during which no wave computes, then two barrier
+// waits.  Here the workgroup's waves split the two jobs:
+//   * NH = 16 - NF hash waves own the keys (one per lane per phase, PER keys
+//     per lane in sweeps): claims, XXH3 of the next key beside them, slot
+//     writes; after the first barrier, the walk of the next key's positions
+//     (VALU only, beside the flush);
+//   * NF flush waves own the bins, BPL consecutive bins per lane (one
+//     ds_read_b128 of their fill words): after the first barrier they post
+//     every full segment of their bins into their own job table (dense: up
+//     to 16 segments per store instruction, so ~half the store instructions
+//     of a table per wave of 57 owners), write the segments with the
+//     cooperative 4-lane stores and advance their rings.
+// The same rings, fill words, regions and overflow paths as k_bin; pass B
+// and the region layout are unchanged.
+template <int NF>
+struct Bin2Geo {
+    static constexpr int NH = kBinBlock / 64 - NF;           // hash waves
+    static constexpr uint32_t KPP = NH * 64;                 // key slots per phase (per PER)
+    static constexpr uint32_t BPL = kMaxBinsPerSweep / (NF * 64);  // bins per flush lane
+    static constexpr uint32_t kJobs = 80;                    // job-table entries per flush wave (last: scratch)
+    static_assert(BPL == 4 || BPL == 8, "flush lanes read their fill words as uint4");
+};
+// LDS bytes of k_bin2: rings of nb + 1 slices, fill words for every flush-lane
+// bin (+ the sink), job tables.
+template <int NF>
+constexpr size_t bin2_lds_bytes(uint32_t nb, uint32_t ring) {
+    return ((((size_t)(nb + 1) * ring) + 3) & ~(size_t)3) * 4 + (kMaxBinsPerSweep + 4) * 4 +
+           (size_t)NF * Bin2Geo<NF>::kJobs * 16;
+}
+
+template <class Src, class W, int KMAX, bool FULL, int PER, int SL, int NF>
+__global__ __launch_bounds__(kBinBlock) void k_bin2(Src src, uint64_t n, Mod32 md, uint32_t, PassA a) {
+    using G = Bin2Geo<NF>;
+    constexpr int NH = G::NH;
+    constexpr uint32_t KPP = G::KPP, BPL = G::BPL, kJobs = G::kJobs, kPost = kJobs - 1;
+    constexpr uint32_t kMask = (1u << SL) - 1;
+    constexpr int NP = PER * KMAX;
+    extern __shared__ uint32_t sm[];
+    const uint32_t R = a.ring, R4 = 4 * a.ring, nb = a.nb;
+    uint32_t* fill = sm + ((((size_t)(nb + 1) * R) + 3) & ~(size_t)3);  // [kMaxBinsPerSweep + 4]
+    uint4* jobtab = reinterpret_cast<uint4*>(fill + kMaxBinsPerSweep + 4);
+    const uint32_t tid = threadIdx.x, w = blockIdx.x, lane = tid & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: the role branches are uniform
+    for (uint32_t i = tid; i < kMaxBinsPerSweep + 4; i += kBinBlock) fill[i] = 0;
+    constexpr uint32_t kInc = 4u | (1u << 16);
+    const uint32_t sink = nb << SL;
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t i0 = (uint64_t)w * per, i1 = min(n, i0 + per);
+    const uint64_t iters = i1 > i0 ? (i1 - i0 + PER * KPP - 1) / (PER * KPP) : 0;  // uniform
+    const uint64_t groups = (iters + kAhead - 1) / kAhead;  // phases run in whole groups of kAhead
+    __syncthreads();
+#if LSMB_STAMP
+    uint64_t st_sum[4] = {0, 0, 0, 0}, st_prev = stamp(), st_t;
+#define LSMB_ST(q) (st_t = stamp(), st_sum[q] += st_t - st_prev, st_prev = st_t)
+#else
+#define LSMB_ST(q) ((void)0)
+#endif
+    // The two roles run separate loops with the same barriers (two per
+    // phase, the same number of phases), so each keeps only its own state in
+    // registers.
+    if (wave < (uint32_t)NH) {
+        // ------------------------------------------------ hash waves
+        const uint32_t lim = R << 16;
+        const uint32_t hl = wave * 64 + lane;
+        auto key_index = [&](uint64_t it) { return i0 + (it * KPP + hl) * PER; };
+        auto key_ok = [&](uint64_t it, int j = 0) { return it < iters && key_index(it) + j < i1; };
+        using Pre = typename Src::Pre;
+        auto fetch_keys = [&](uint64_t it, Pre (&out)[PER]) {
+#pragma unroll
+            for (int j = 0; j < PER; j++) out[j] = src.fetch(key_index(it) + j, key_ok(it, j));
+        };
+        auto walk_positions = [&](const typename Src::Seed& h, bool ok, uint32_t* out) {
+            W walk(md, h);
+#pragma unroll
+            for (int q = 0; q < KMAX; q++) {
+                const uint32_t lp = walk.pos() - (FULL ? 0u : (a.b0 << SL));
+                out[q] = (FULL || lp < sink) ? lp : sink;
+                if (q + 1 < KMAX) walk.next(md);
+            }
+            if (__builtin_expect(__ballot(!ok) != 0, 0)) {
+#pragma unroll
+                for (int q = 0; q < KMAX; q++)
+                    if (!ok) out[q] = sink;
+            }
+        };
+        uint32_t pos[NP], kinc[PER];
+        Pre pb0[PER], pb1[PER], pb2[PER], pb3[PER];
+#pragma unroll
+        for (int j = 0; j < PER; j++) {
+            const bool ok = key_ok(0, j);
+            const Pre p = src.fetch(key_index(0) + j, ok);
+            const typename Src::Seed h = ok ? src.hash_pre(p, key_index(0) + j) : typename Src::Seed{};
+            walk_positions(h, ok, pos + j * KMAX);
+            kinc[j] = ok ? kInc : 0u;
+        }
+        fetch_keys(1, pb1);
+        fetch_keys(2, pb2);
+        fetch_keys(3, pb3);
+        fetch_keys(4, pb0);
+        auto phase = [&](uint64_t it, Pre (&pre)[PER]) __attribute__((always_inline)) {
+            // claims, back to back
+            uint32_t got[NP];
+#pragma unroll
+            for (int q = 0; q < NP; q++) {
+                if (FULL)
+                    got[q] = atomicAdd(fill + (pos[q] >> SL), kinc[q / KMAX]);
+                else
+                    got[q] = pos[q] < sink ? atomicAdd(fill + (pos[q] >> SL), kInc) : 0u;
+            }
+            // XXH3 of the next key while they are in flight (pinned here)
+            typename Src::Seed nh[PER];
+            bool nok[PER];
+#pragma unroll
+            for (int j = 0; j < PER; j++) {
+                nok[j] = key_ok(it + 1, j);
+                nh[j] = src.hash_pre(pre[j], key_index(it + 1) + j);
+            }
+            fetch_keys(it + 1 + kAhead, pre);
+#pragma unroll
+            for (int j = 0; j < PER; j++) pin_seed(nh[j]);
+            // slot writes (fast path: no claim of the wave past its ring)
+            uint32_t gmax = 0;
+#pragma unroll
+            for (int q = 0; q < NP; q++) gmax = max(gmax, got[q]);
+            auto slot = [&](int q) {
+                uint32_t x = got[q] & 0xFFFFu;
+                x = min(x, x - R4);
+                return __umul24(pos[q] >> SL, R4) + x;
+            };
+            if (__builtin_expect(__ballot(gmax >= lim) == 0, 1)) {
+#pragma unroll
+                for (int q = 0; q < NP; q++)
+                    if (FULL || pos[q] < sink) *(uint32_t*)((char*)sm + slot(q)) = pos[q] & kMask;
+            } else {
+#pragma unroll
+                for (int q = 0; q < NP; q++) {
+                    if (FULL || pos[q] < sink) {
+                        if (got[q] < lim)
+                            *(uint32_t*)((char*)sm + slot(q)) = pos[q] & kMask;
+                        else if (pos[q] < sink)
+                            or_pos_global<SL>(a.gw, a.b0 + (pos[q] >> SL), pos[q] & kMask);
+                    }
+                }
+            }
+            LSMB_ST(0);
+            lds_barrier();
+            LSMB_ST(1);
+            // the next key's positions (VALU only), beside the flush waves
+#pragma unroll
+            for (int j = 0; j < PER; j++) {
+                walk_positions(nh[j], nok[j], pos + j * KMAX);
+                kinc[j] = nok[j] ? kInc : 0u;
+            }
+#pragma unroll
+            for (int q = 0; q < NP; q++) asm volatile("" ::"v"(pos[q]));
+            LSMB_ST(2);
+            lds_barrier();
+            LSMB_ST(3);
+        };
+        for (uint64_t g = 0; g < groups; g++) {
+            const uint64_t it = g * kAhead;
+            phase(it, pb1);
+            phase(it + 1, pb2);
+            phase(it + 2, pb3);
+            phase(it + 3, pb0);
+        }
+        return;
+    }
+    // ------------------------------------------------ flush waves
+    const __amdgpu_buffer_rsrc_t rgn = __builtin_amdgcn_make_buffer_rsrc(
+        region_ptr(a, 0, w), 0, (int)(a.nbins * a.cap * 64u), 0x00020000);
+    constexpr uint32_t kDrop = 0x80000000u;
+    const uint32_t fw = wave - NH, fl = fw * 64 + lane, fb0 = fl * BPL;  // this lane's bins fb0 ..
+    // A bin's ring start is not kept: its fill word holds start + 4 * claims
+    // (lo16) and claims (hi16), so start = lo16 - 4 * hi16 (mod 4R).
+    auto ring_start = [&](uint32_t f) {
+        const uint32_t s = (f & 0xFFFFu) - 4 * (f >> 16);
+        return min(s, s + R4);
+    };
+    uint32_t segs[BPL];  // region segments written, per bin
+#pragma unroll
+    for (uint32_t m = 0; m < BPL; m++) segs[m] = 0;
+    for (uint64_t ph = 0; ph < groups * kAhead; ph++) {
+        LSMB_ST(0);
+        lds_barrier();
+        LSMB_ST(1);
+        // fill words of this lane's bins (bins >= nb: the sink's and the
+        // padding's, which stay 0)
+        uint32_t fv[BPL];
+#pragma unroll
+        for (uint32_t m = 0; m < BPL; m += 4) {
+            const uint4 v = *(const uint4*)(fill + fb0 + m);
+            fv[m] = v.x, fv[m + 1] = v.y, fv[m + 2] = v.z, fv[m + 3] = v.w;
+        }
+        uint32_t cnt[BPL], start[BPL];
+        bool has[BPL], posted[BPL];
+        uint32_t base = 0;
+#pragma unroll
+        for (uint32_t m = 0; m < BPL; m++) {
+            const uint32_t b = fb0 + m;
+            start[m] = ring_start(fv[m]);
+            cnt[m] = b < nb ? min(fv[m] >> 16, R) : 0u;
+            has[m] = cnt[m] >= (uint32_t)kSegEntries;
+            const bool coop = has[m] && segs[m] < a.cap;
+            const uint64_t cm = __ballot(coop);
+            const uint32_t jr =
+                base + __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
+            posted[m] = coop && jr < kPost;
+            uint32_t g1 = start[m] + 32, g2 = start[m] + 64;
+            g1 = min(g1, g1 - R4);
+            g2 = min(g2, g2 - R4);
+            const uint32_t rb = min(b, nb) * R4;  // (padding bins: the sink's ring, in bounds)
+            jobtab[fw * kJobs + (posted[m] ? jr : kPost)] =
+                make_uint4(rb + start[m], rb + g1, rb + g2, ((a.b0 + b) * a.cap + segs[m]) * 64u);
+            base += (uint32_t)__popcll(cm);
+        }
+        const uint32_t jobs = min(base, kPost);  // wave-uniform
+        // cooperative stores: lane L writes 16 B of job r*16 + L/4
+        for (uint32_t r = 0; r * 16 < jobs; r++) {
+            const uint32_t j = r * 16 + (lane >> 2), l = lane & 3;
+            const bool valid = j < jobs;
+            const uint4 jb = jobtab[fw * kJobs + (valid ? j : kPost)];
+            const uint2 a0 = *(const uint2*)((const char*)sm + jb.x + 8 * l);
+            const uint2 a1 = *(const uint2*)((const char*)sm + jb.y + 8 * l);
+            const uint2 a2 = *(const uint2*)((const char*)sm + jb.z + 8 * l);
+            const uint2 w0 = pack3w<SL>(a0.x, a1.x, a2.x), w1 = pack3w<SL>(a0.y, a1.y, a2.y);
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{w0.x, w0.y, w1.x, w1.y}, rgn, valid ? jb.w + 16 * l : kDrop, 0,
+                                                   LSMB_STORE_AUX);
+        }
+        // advance the rings; a second segment of a bin, or an unposted one
+        // (full region / full table), per lane (rare)
+        bool rare = false;
+#pragma unroll
+        for (uint32_t m = 0; m < BPL; m++) rare |= has[m] && (!posted[m] || cnt[m] >= 2u * kSegEntries);
+        if (__builtin_expect(__ballot(rare) != 0, 0)) {
+            for (uint32_t m = 0; m < BPL; m++) {
+                if (!has[m]) continue;
+                const uint32_t b = fb0 + m;
+                const char* ring = (const char*)sm + b * R4;
+                const uint32_t nf = cnt[m] / (uint32_t)kSegEntries;
+                for (uint32_t j = 0; j < nf; j++) {
+                    if (j > 0 || !posted[m]) {  // this segment per lane
+                        uint32_t g1 = start[m] + 32, g2 = start[m] + 64;
+                        g1 = min(g1, g1 - R4);
+                        g2 = min(g2, g2 - R4);
+                        uint32_t v[kSegEntries];
+                        for (int t = 0; t < 8; t++) {
+                            v[t] = *(const uint32_t*)(ring + start[m] + 4 * t);
+                            v[t + 8] = *(const uint32_t*)(ring + g1 + 4 * t);
+                            v[t + 16] = *(const uint32_t*)(ring + g2 + 4 * t);
+                        }
+                        if (segs[m] < a.cap) {
+                            uint64_t* dst = region_ptr(a, a.b0 + b, w) + (uint64_t)segs[m] * kSegWords;
+                            for (int t = 0; t < kSegWords; t++) dst[t] = pack3<SL>(v[t], v[t + 8], v[t + 16]);
+                        } else {
+                            for (int t = 0; t < kSegEntries; t++) or_pos_global<SL>(a.gw, a.b0 + b, v[t]);
+                        }
+                    }
+                    uint32_t s2 = start[m] + 96;
+                    start[m] = min(s2, s2 - R4);
+                    segs[m] = min(segs[m] + 1, a.cap);
+                }
+                const uint32_t rem = cnt[m] - nf * (uint32_t)kSegEntries;
+                fv[m] = (start[m] + 4 * rem) | (rem << 16);
+            }
+        } else {
+#pragma unroll
+            for (uint32_t m = 0; m < BPL; m++) {
+                uint32_t s2 = start[m] + 96;
+                s2 = min(s2, s2 - R4);
+                const uint32_t rem = cnt[m] - (uint32_t)kSegEntries;
+                fv[m] = has[m] ? ((s2 + 4 * rem) | (rem << 16)) : fv[m];
+                segs[m] = has[m] ? segs[m] + 1 : segs[m];
+            }
+        }
+#pragma unroll
+        for (uint32_t m = 0; m < BPL; m += 4)
+            *(uint4*)(fill + fb0 + m) = make_uint4(fv[m], fv[m + 1], fv[m + 2], fv[m + 3]);
+        LSMB_ST(2);
+        lds_barrier();
+        LSMB_ST(3);
+    }
+#if LSMB_STAMP
+    if (lane == 0) {  // the flush waves' view of the phase
+        for (int q = 0; q < 4; q++) atomicAdd(&g_stamp[q], (unsigned long long)st_sum[q]);
+        atomicAdd(&g_stamp[4], (unsigned long long)groups * kAhead);
+        atomicAdd(&g_stamp[5], 1ull);
+    }
+#endif
+#undef LSMB_ST
+    // leftovers: each bin's open segment (padded with its first entry), then
+    // the region's segment count
+#pragma unroll
+    for (uint32_t m = 0; m < BPL; m++) {
+        const uint32_t b = fb0 + m;
+        if (b >= nb) continue;
+        const uint32_t fvb = fill[b];
+        uint32_t cnt = min(fvb >> 16, R), start = ring_start(fvb);
+        const char* ring = (const char*)sm + b * R4;
+        while (cnt) {
+            const uint32_t mm = min(cnt, (uint32_t)kSegEntries);
+            uint32_t v[kSegEntries];
+#pragma unroll
+            for (int t = 0; t < kSegEntries; t++) {
+                uint32_t x = start + 4 * ((uint32_t)t < mm ? t : 0);
+                x = min(x, x - R4);
+                v[t] = *(const uint32_t*)(ring + x);
+            }
+            if (segs[m] < a.cap) {
+                uint64_t* dst = region_ptr(a, a.b0 + b, w) + (uint64_t)segs[m] * kSegWords;
+#pragma unroll
+                for (int t = 0; t < kSegWords; t++) dst[t] = pack3<SL>(v[t], v[t + 8], v[t + 16]);
+                segs[m]++;
+            } else {
+                for (uint32_t t = 0; t < mm; t++) or_pos_global<SL>(a.gw, a.b0 + b, v[t]);
+            }
+            uint32_t x = start + 4 * mm;
+            start = min(x, x - R4);
+            cnt -= mm;
+        }
+        a.counts[(uint64_t)(a.b0 + b) * a.grid + w] = segs[m];
     }
 }
 
@@ -718,15 +1069,15 @@ __global__ __launch_bounds__(256) void k_gen_splitmix(uint64_t seed, uint64_t fi
     }
 }
 
-// (h1, h2) = xxh3_128(key i) for every key, as 16-B records (ks::Hashed).
-// Full occupancy and no barriers, so the per-lane key-byte loads of many
-// waves overlap; pass A then reads 16 coalesced bytes per key.
-template <class Src>
-__global__ __launch_bounds__(256) void k_hash(Src src, uint64_t n, uint4* __restrict__ out) {
+// (h1, h2) = xxh3_128(key i) for every key, as 16-B records (ks::Hashed) or
+// 12-B walk records (ks::Recs).  Full occupancy and no barriers, so the
+// per-lane key-byte loads of many waves overlap; pass A then reads
+// coalesced records.
+template <class Src, class Out>
+__global__ __launch_bounds__(256) void k_hash(Src src, uint64_t n, Out out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const H128 h = src.hash(i);
-    out[i] = make_uint4((uint32_t)h.lo, (uint32_t)(h.lo >> 32), (uint32_t)h.hi, (uint32_t)(h.hi >> 32));
+    out.put(i, src.hash(i));
 }
 
 // The max-dynamic-LDS attribute is a property of the kernel, not of a launch:
@@ -749,9 +1100,10 @@ void set_max_lds(const void* fn) {
 #ifndef LSMB_HV_WIN
 #define LSMB_HV_WIN (36 * 1024)
 #endif
-void launch_hash_var(const VarLen& src, uint64_t n, uint4* out, hipStream_t st) {
+template <class Out>
+void launch_hash_var(const VarLen& src, uint64_t n, Out out, hipStream_t st) {
     const uint64_t g = (n + LSMB_HV_KEYS - 1) / LSMB_HV_KEYS;
-    k_hash_var<0, LSMB_HV_KEYS, LSMB_HV_WIN><<<dim3((uint32_t)g), dim3(LSMB_HV_KEYS), 0, st>>>(src.d, src.o, n, out);
+    k_hash_var<0, LSMB_HV_KEYS, LSMB_HV_WIN, 0, Out><<<dim3((uint32_t)g), dim3(LSMB_HV_KEYS), 0, st>>>(src.d, src.o, n, out);
 }
 
 template <class Src>
@@ -764,7 +1116,11 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
     if (sweep > 0 && s != BuildStrategy::Partition) return hipSuccess;
     const uint32_t nw32 = (uint32_t)(2 * (((uint64_t)num_bits + 63) / 64));
     if (tm && !t0_done) hipEventRecord(tm->t0, st);
-    if (s == BuildStrategy::Lds) {
+    constexpr bool kRecSrc = std::is_same<Src, ks::Recs>::value;  // walk records: partition builds only
+    if (s != BuildStrategy::Partition) {
+      if constexpr (kRecSrc) {
+        return hipErrorInvalidValue;
+      } else if (s == BuildStrategy::Lds) {
         const size_t smem = (size_t)nw32 * 4;
         // ~8 Ki keys per workgroup keeps the final per-word OR cheap.
         uint64_t g = (n + 8191) / 8192;
@@ -784,9 +1140,9 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
             const uint64_t g = (n + 255) / 256;
             if (g > 0x7FFFFFFFull) return hipErrorInvalidValue;
             if constexpr (std::is_same<Src, VarLen>::value)
-                launch_hash_var(src, n, ws.hashes, st);
+                launch_hash_var(src, n, OutH128(ws.hashes), st);
             else
-                k_hash<Src><<<dim3((uint32_t)g), dim3(256), 0, st>>>(src, n, ws.hashes);
+                k_hash<Src, OutH128><<<dim3((uint32_t)g), dim3(256), 0, st>>>(src, n, OutH128(ws.hashes));
             const Hashed hs{ws.hashes};
             set_max_lds((const void*)k_build_tiled<Hashed>);
             k_build_tiled<Hashed><<<dim3(tp.chunks * tp.nslices), dim3(1024), kSliceWords32 * 4, st>>>(
@@ -804,20 +1160,29 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
         if (g > (uint64_t)num_cus * 8) g = (uint64_t)num_cus * 8;
         k_build_atomic<Src><<<dim3((uint32_t)g), dim3(256), 0, st>>>(src, n, md, k, gw);
         if (tm) hipEventRecord(tm->t1, st);
+      }
     } else if constexpr (Src::kPrehash) {
-        if (ws.hash_bytes < n * 16) return hipErrorInvalidValue;
+        // hashed first, into 12-B walk records (pass A then walks without
+        // the reductions; partition builds have k <= 32)
+        if (ws.hash_bytes < n * 12) return hipErrorInvalidValue;
         const uint64_t g = (n + 255) / 256;
         if (g > 0x7FFFFFFFull) return hipErrorInvalidValue;
+        const OutRec rec{reinterpret_cast<uint32_t*>(ws.hashes), md, k};
         if constexpr (std::is_same<Src, VarLen>::value)
-            launch_hash_var(src, n, ws.hashes, st);
+            launch_hash_var(src, n, rec, st);
         else
-            k_hash<Src><<<dim3((uint32_t)g), dim3(256), 0, st>>>(src, n, ws.hashes);
+            k_hash<Src, OutRec><<<dim3((uint32_t)g), dim3(256), 0, st>>>(src, n, rec);
         // pass A's timer (t1) covers k_hash + k_bin
-        return build_with(Hashed{ws.hashes}, n, num_bits, k, gw, s, ws, num_cus, st, tm, sweep, /*t0_done=*/true);
+        return build_with(ks::Recs{reinterpret_cast<const uint32_t*>(ws.hashes)}, n, num_bits, k, gw, s, ws, num_cus,
+                          st, tm, sweep, /*t0_done=*/true);
     } else {
         const PartitionPlan pl = plan_partition(num_bits, k, n, num_cus);
         if (pl.region_bytes > ws.region_bytes || pl.counts_bytes > ws.counts_bytes) return hipErrorInvalidValue;
         const bool w32 = fits_walk32(num_bits);
+        // walks: from (h1, h2), or replayed from 12-B records
+        constexpr bool kRec = std::is_same<Src, ks::Recs>::value;
+        using Walk32 = std::conditional_t<kRec, RecWalk32, lsmb::Walk32>;
+        using Walk64 = std::conditional_t<kRec, RecWalk64, lsmb::Walk64>;
         for (uint32_t sw = 0; sw < pl.sweeps; sw++) {
             if (sweep >= 0 && sw != (uint32_t)sweep) continue;
             PassA a;
@@ -837,9 +1202,36 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
                 kern<<<dim3(pl.grid), dim3(kBinBlock), smem, st>>>(src, n, md, k, a);
             };
             const bool full = pl.sweeps == 1;
+            // k_bin2 (specialised hash / flush waves) where its LDS fits;
+            // LSMB_BIN2=0 selects k_bin (measurement knob)
+            static const int bin2_env = [] {
+                const char* e = getenv("LSMB_BIN2");
+                return e ? atoi(e) : 1;
+            }();
+            constexpr int NF = 4;
+            const size_t smem2 = bin2_lds_bytes<NF>(a.nb, a.ring);
+            const bool use2 = bin2_env != 0 && smem2 <= kLdsBytes;
+            auto go2 = [&](auto kern) {
+                set_max_lds((const void*)kern);
+                kern<<<dim3(pl.grid), dim3(kBinBlock), smem2, st>>>(src, n, md, k, a);
+            };
             auto go7 = [&](auto slc) {  // k = 7 (BloomFilter::new at fpr 0.01), bin width 2^SL
                 constexpr int SL = decltype(slc)::value;
                 const bool two = pl.keys_per_lane == 2;
+                if (use2) {
+                    if (w32) {
+                        if (full && two) go2(k_bin2<Src, Walk32, 7, true, 2, SL, NF>);
+                        else if (full) go2(k_bin2<Src, Walk32, 7, true, 1, SL, NF>);
+                        else if (two) go2(k_bin2<Src, Walk32, 7, false, 2, SL, NF>);
+                        else go2(k_bin2<Src, Walk32, 7, false, 1, SL, NF>);
+                    } else {
+                        if (full && two) go2(k_bin2<Src, Walk64, 7, true, 2, SL, NF>);
+                        else if (full) go2(k_bin2<Src, Walk64, 7, true, 1, SL, NF>);
+                        else if (two) go2(k_bin2<Src, Walk64, 7, false, 2, SL, NF>);
+                        else go2(k_bin2<Src, Walk64, 7, false, 1, SL, NF>);
+                    }
+                    return;
+                }
                 if (w32) {
                     if (full && two) go(k_bin<Src, Walk32, 7, true, true, 2, SL>);
                     else if (full) go(k_bin<Src, Walk32, 7, true, true, 1, SL>);
@@ -865,6 +1257,21 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
+#if LSMB_STAMP
+        {
+            unsigned long long h[8];
+            hipStreamSynchronize(st);
+            hipMemcpyFromSymbol(h, HIP_SYMBOL(g_stamp), sizeof h);
+            const double ph = (double)h[4] ? (double)h[4] : 1.0;  // wave-phases
+            const double tot = (double)(h[0] + h[1] + h[2] + h[3]);
+            fprintf(stderr, "[stamp] waves %llu phases/wave %.1f cycles/phase %.0f: work %.0f (%.1f%%) b1 %.0f (%.1f%%) "
+                            "flush %.0f (%.1f%%) b2 %.0f (%.1f%%)\n",
+                    h[5], ph / (double)h[5], tot / ph, h[0] / ph, 100 * h[0] / tot, h[1] / ph, 100 * h[1] / tot,
+                    h[2] / ph, 100 * h[2] / tot, h[3] / ph, 100 * h[3] / tot);
+            const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), z, sizeof z);
+        }
+#endif
         if (tm) hipEventRecord(tm->t1, st);
         const uint32_t bfirst = sweep >= 0 ? (uint32_t)sweep * pl.bins_per_sweep : 0u;
         const uint32_t bend = sweep >= 0 ? min(pl.nbins, bfirst + pl.bins_per_sweep) : pl.nbins;

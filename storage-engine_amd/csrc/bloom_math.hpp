@@ -122,6 +122,7 @@ struct Walk32T {
         const uint32_t t = s0 + md.dt;  // < 2d <= 2^32
         s1 = t - md.d < t ? t - md.d : t;
     }
+    LSMB_HD Walk32T(const M& md, const H128& h) : Walk32T(md, h.lo, h.hi) {}
     LSMB_HD uint32_t pos() const { return r; }
     LSMB_HD void next(const M&) {
         uint64_t nx;
@@ -145,6 +146,7 @@ struct Walk64 {
         r = md.reduce(h1);
         s = md.reduce(h2_);
     }
+    LSMB_HD Walk64(const Mod32& md, const H128& h) : Walk64(md, h.lo, h.hi) {}
     LSMB_HD uint32_t pos() const { return r; }
     LSMB_HD void next(const Mod32& md) {
         uint64_t nx;
@@ -159,6 +161,59 @@ struct Walk64 {
 
 // The 64-bit-safe walk, used where d may exceed 2^31.
 using PosWalk = Walk64;
+
+// A key's walk reduced to 12 bytes, for builds that hash in a separate kernel
+// (variable-length and odd-length keys): r = h1 mod d, s = h2 mod d and the
+// carries c_i of the wrapping sums h1 + i*h2 (bit i-1 = carry out of
+// x_{i-1} + h2, i = 1 .. 31).  The walks below replay Walk32 / Walk64 from it
+// exactly (tests: every C4 build against the oracle), without the two
+// reductions and the 64-bit sums in the pass that consumes it.
+struct WalkRec {
+    uint32_t r, s, c;
+
+    static LSMB_HD WalkRec make(const Mod32& md, const H128& h, uint32_t k) {
+        WalkRec q;
+        q.r = md.reduce(h.lo);
+        q.s = md.reduce(h.hi);
+        q.c = 0;
+        uint64_t x = h.lo;
+        for (uint32_t i = 0; i + 1 < k && i < 31; i++) {
+            uint64_t nx;
+            if (__builtin_add_overflow(x, h.hi, &nx)) q.c |= 1u << i;
+            x = nx;
+        }
+        return q;
+    }
+};
+
+struct RecWalk32 {  // d <= 2^31, as Walk32
+    using Mod = Mod32;
+    uint32_t r, s0, s1, c, d;
+    LSMB_HD RecWalk32(const Mod32& md, const WalkRec& q) : r(q.r), s0(q.s), c(q.c), d(md.d) {
+        const uint32_t t = s0 + md.dt;
+        s1 = t - md.d < t ? t - md.d : t;
+    }
+    LSMB_HD uint32_t pos() const { return r; }
+    LSMB_HD void next(const Mod32&) {
+        const uint32_t u = r + ((c & 1u) ? s1 : s0);
+        c >>= 1;
+        r = u - d < u ? u - d : u;
+    }
+};
+
+struct RecWalk64 {  // any d < 2^32, as Walk64
+    using Mod = Mod32;
+    uint32_t r, s, c;
+    LSMB_HD RecWalk64(const Mod32&, const WalkRec& q) : r(q.r), s(q.s), c(q.c) {}
+    LSMB_HD uint32_t pos() const { return r; }
+    LSMB_HD void next(const Mod32& md) {
+        uint64_t u = (uint64_t)r + s;
+        if (u >= md.d) u -= md.d;
+        if (c & 1u) u = (u >= md.t64) ? u - md.t64 : u + md.dt;
+        c >>= 1;
+        r = (uint32_t)u;
+    }
+};
 
 LSMB_HD bool fits_walk32(uint32_t d) { return d <= 0x80000000u; }
 

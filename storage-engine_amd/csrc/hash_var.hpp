@@ -52,11 +52,32 @@ __device__ __forceinline__ uint32_t len_class(uint64_t len) {
     return 9;
 }
 
+// Where a hash kernel puts key i's hash: the 16-B (h1, h2) record (filter
+// tiles, tools), or the 12-B walk record of a partitioned build (WalkRec:
+// h1 and h2 reduced mod num_bits plus the walk's carries).
+struct OutH128 {
+    uint4* p;
+    __host__ __device__ OutH128(uint4* q) : p(q) {}
+    __device__ __forceinline__ void put(uint64_t i, const H128& h) const {
+        p[i] = make_uint4((uint32_t)h.lo, (uint32_t)(h.lo >> 32), (uint32_t)h.hi, (uint32_t)(h.hi >> 32));
+    }
+};
+struct OutRec {
+    uint32_t* p;
+    Mod32 md;
+    uint32_t k;
+    __device__ __forceinline__ void put(uint64_t i, const H128& h) const {
+        const WalkRec q = WalkRec::make(md, h, k);
+        uint32_t* o = p + 3 * i;
+        o[0] = q.r, o[1] = q.s, o[2] = q.c;
+    }
+};
+
 // WPE: waves per SIMD the register allocation must allow (0: compiler's
 // choice).  The hash paths want ~130 VGPRs; at <= 128 four waves fit a SIMD.
-template <int MODE = 0, uint32_t KEYS = kHashKeys, uint32_t WIN = kHashWin, int WPE = 0>
+template <int MODE = 0, uint32_t KEYS = kHashKeys, uint32_t WIN = kHashWin, int WPE = 0, class Out = OutH128>
 __global__ __launch_bounds__(KEYS) __attribute__((amdgpu_waves_per_eu(WPE ? WPE : 1)))
-void k_hash_var(const uint8_t* __restrict__ d, const uint64_t* __restrict__ o, uint64_t n, uint4* __restrict__ out) {
+void k_hash_var(const uint8_t* __restrict__ d, const uint64_t* __restrict__ o, uint64_t n, Out out) {
     constexpr uint32_t kPieces = WIN / (KEYS * 16);  // 16-B loads per thread per round
     static_assert(kPieces * KEYS * 16 == WIN, "window must be a whole number of rounds of loads");
     __shared__ uint32_t win[WIN / 4 + 8];
@@ -120,7 +141,7 @@ void k_hash_var(const uint8_t* __restrict__ d, const uint64_t* __restrict__ o, u
             f += c;
         }
     }
-    if (j < m) out[i0 + j] = make_uint4((uint32_t)h.lo, (uint32_t)(h.lo >> 32), (uint32_t)h.hi, (uint32_t)(h.hi >> 32));
+    if (j < m) out.put(i0 + j, h);
 }
 
 }  // namespace lsmb

@@ -19,6 +19,7 @@ namespace ks {
 // past the caches (each key is read exactly once).
 struct Fixed16 {
     static constexpr bool kPrehash = false;  // hashed inline by pass A
+    using Seed = H128;  // what hash_pre returns: the walk's start
     const uint4* k;
     __device__ __forceinline__ H128 hash(uint64_t i) const {
         uint4 v = ld_stream16(k + i);
@@ -39,6 +40,7 @@ struct Fixed16 {
 // Any fixed key length, any alignment.
 struct FixedN {
     static constexpr bool kPrehash = true;  // partitioned builds hash in k_hash first
+    using Seed = H128;
     const uint8_t* d;
     uint32_t len;
     __device__ __forceinline__ H128 hash(uint64_t i) const { return xxh3_128(d + i * len, len); }
@@ -52,6 +54,7 @@ struct FixedN {
 // Packed variable-length keys: key i = d[o[i] .. o[i+1]).
 struct VarLen {
     static constexpr bool kPrehash = true;  // partitioned builds hash in k_hash first
+    using Seed = H128;
     const uint8_t* d;
     const uint64_t* o;
     __device__ __forceinline__ H128 hash(uint64_t i) const {
@@ -75,6 +78,7 @@ struct VarLen {
 // latency of every key-byte load and the length-class divergence of XXH3.
 struct Hashed {
     static constexpr bool kPrehash = false;
+    using Seed = H128;
     const uint4* h;
     __device__ __forceinline__ H128 hash(uint64_t i) const { return hash_pre(ld_stream16(h + i), i); }
     using Pre = uint4;
@@ -86,5 +90,28 @@ struct Hashed {
     }
 };
 
+// 12-B walk records (WalkRec) written by k_hash / k_hash_var for a
+// partitioned build: pass A reads three coalesced dwords per key and walks
+// without reductions (RecWalk32 / RecWalk64).
+struct Recs {
+    static constexpr bool kPrehash = false;
+    using Seed = WalkRec;
+    const uint32_t* q;  // 3 u32 per key
+    using Pre = WalkRec;
+    __device__ __forceinline__ Pre fetch(uint64_t i, bool ok) const {
+        if (!ok) return WalkRec{0, 0, 0};
+        const uint32_t* p = q + 3 * i;
+        return WalkRec{__builtin_nontemporal_load(p), __builtin_nontemporal_load(p + 1),
+                       __builtin_nontemporal_load(p + 2)};
+    }
+    __device__ __forceinline__ WalkRec hash_pre(const Pre& v, uint64_t) const { return v; }
+};
+
 }  // namespace ks
+
+// Register pins (an empty asm consuming the value) for a walk seed.
+__device__ __forceinline__ void pin_seed(const H128& h) {
+    asm volatile("" ::"v"((uint32_t)h.lo), "v"((uint32_t)(h.lo >> 32)), "v"((uint32_t)h.hi), "v"((uint32_t)(h.hi >> 32)));
+}
+__device__ __forceinline__ void pin_seed(const WalkRec& q) { asm volatile("" ::"v"(q.r), "v"(q.s), "v"(q.c)); }
 }  // namespace lsmb

@@ -215,3 +215,19 @@ def test_sweep_ranges_tile_the_filter():
         assert at == lsmbloom.num_words(nb)
         with pytest.raises(ValueError):
             lsmbloom.sweep_words(nb, n, ns, k)
+
+
+def test_walk_records_replay_the_walks(tmp_path):
+    """12-B walk records (WalkRec: h1, h2 mod num_bits + the walk's carries),
+    which k_hash / k_hash_var write for partitioned var-len and odd-length
+    builds, replay Walk32 / Walk64 exactly, and both equal the literal
+    (h1 +wrap i*h2) % num_bits of src/bloom/mod.rs:192-197 (host build of the
+    device header; 200 k random and edge-case (h1, h2, num_bits, k))."""
+    import subprocess
+    exe = str(tmp_path / "walkrec_test")
+    src = os.path.join(ROOT, "tests", "cpp", "walkrec_test.cpp")
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "--offload-arch=gfx950", src, "-o", exe],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr

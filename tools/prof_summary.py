@@ -18,27 +18,33 @@ def short(name):
 
 
 def traffic_json(d, out):
-    """Per-dispatch HBM bytes of the C2 build kernels (k_bin<Fixed16...> +
-    k_apply) -> JSON read by bench.py (roofline.traffic)."""
+    """Per-dispatch HBM bytes and VALU instructions of the C2 build kernels
+    (pass A k_bin / k_bin2 <Fixed16...> + pass B k_apply) -> JSON read by
+    bench.py (roofline.traffic, roofline.secondary)."""
     import json
     per = collections.defaultdict(dict)
-    for sub, cn in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+    for sub, cns in (("fetch", ("FETCH_SIZE",)), ("write", ("WRITE_SIZE",)), ("sq2", ("SQ_INSTS_VALU",))):
         p = os.path.join(d, sub, "run_counter_collection.csv")
-        vals = collections.defaultdict(list)
+        if not os.path.exists(p):
+            continue
+        vals = collections.defaultdict(lambda: collections.defaultdict(list))
         for r in csv.DictReader(open(p)):
-            if r["Counter_Name"] == cn:
-                vals[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
-        for kn, v in vals.items():
-            per[kn][cn] = sum(v) / len(v)
+            if r["Counter_Name"] in cns:
+                vals[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for kn, cv in vals.items():
+            for cn, v in cv.items():
+                per[kn][cn] = sum(v) / len(v)
     kern = {}
     for kn, m in per.items():
-        if kn.startswith("k_bin<ks::Fixed16") or kn.startswith("k_apply"):
+        if kn.startswith(("k_bin<ks::Fixed16", "k_bin2<ks::Fixed16")) or kn.startswith("k_apply"):
             kern[kn] = {"read_bytes": int(2 * m.get("FETCH_SIZE", 0) * 1024),
-                        "write_bytes": int(m.get("WRITE_SIZE", 0) * 1024)}
+                        "write_bytes": int(m.get("WRITE_SIZE", 0) * 1024),
+                        "valu_insts": int(m.get("SQ_INSTS_VALU", 0))}
     tot = sum(v["read_bytes"] + v["write_bytes"] for v in kern.values())
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench  # the sha of the build kernels' sources this profile measured
     json.dump({"profile": os.path.basename(d.rstrip("/")), "build_bytes": tot, "kernels": kern,
+               "build_valu_insts": sum(v["valu_insts"] for v in kern.values()),
                "kernel_src_sha": bench.build_sources_sha(),
                "note": "FETCH_SIZE x2 (gfx950), KiB -> B; mean per dispatch over separate --pmc passes"},
               open(out, "w"), indent=1)
@@ -46,14 +52,32 @@ def traffic_json(d, out):
 
 def main(d):
     print("# rocprofv3 summary: %s\n" % os.path.basename(d.rstrip("/")))
-    ks = os.path.join(d, "stats", "run_kernel_stats.csv")
-    if os.path.exists(ks):
-        print("## Kernel time (rocprofv3 --kernel-trace --stats)\n")
+    for sub, title in (("stats", "C2 bench"), ("stats_c5", "C5 shard: 125 M keys into 2^32-1 bits"),
+                       ("stats_c4", "C4 var-len build")):
+        ks = os.path.join(d, sub, "run_kernel_stats.csv")
+        if not os.path.exists(ks):
+            continue
+        print("## Kernel time, %s (rocprofv3 --kernel-trace --stats)\n" % title)
         print("| kernel | calls | avg us | total % |")
         print("|---|---|---|---|")
         for r in csv.DictReader(open(ks)):
             print("| %s | %s | %.2f | %.1f |" % (short(r["Name"]), r["Calls"], float(r["AverageNs"]) / 1e3,
                                                 float(r["Percentage"])))
+        print()
+    for sub in ("fetch_c5", "write_c5"):
+        p = os.path.join(d, sub, "run_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        print("## C5 shard, %s (mean per dispatch)\n" % sub.split("_")[0].upper())
+        vals = collections.defaultdict(list)
+        for r in csv.DictReader(open(p)):
+            vals[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+        for kn, v in sorted(vals.items()):
+            if kn.startswith(("k_bin", "k_apply")):
+                m = sum(v) / len(v)
+                mb = (2 if sub.startswith("fetch") else 1) * m * 1024 / 1e6
+                print("- %s: %s = %.4g -> %.1f MB%s" % (kn, sub.split("_")[0].upper() + "_SIZE", m, mb,
+                                                       " (x2, gfx950)" if sub.startswith("fetch") else ""))
         print()
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for sub in ("fetch", "write", "sq1", "sq2"):
