@@ -248,6 +248,9 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
     uint4* jobtab = reinterpret_cast<uint4*>(sm + ((((size_t)(nb + 1) * (R + 1)) + 3) & ~(size_t)3));
     const uint32_t tid = threadIdx.x, w = blockIdx.x, lane = tid & 63, wave = tid >> 6;
     for (uint32_t i = tid; i <= nb; i += kBinBlock) fill[i] = 0;
+    // each wave's scratch job entry (read by the store rounds' idle lanes):
+    // in-bounds ring addresses, a dropped store offset
+    if (lane == 0) jobtab[wave * kBinJobsPerWave + kBinJobsPerWave - 1] = make_uint4(0, 0, 0, 0x80000000u);
     // Workgroup w's regions as a raw buffer: a store at an offset past
     // num_records is dropped by the hardware, which lets every lane issue the
     // flush stores unconditionally (see the flush).
@@ -478,8 +481,8 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
             uint32_t g1 = start + 32, g2 = start + 64;
             g1 = min(g1, g1 - R4);
             g2 = min(g2, g2 - R4);
-            jobtab[wave * kBinJobsPerWave + (posted ? jr : kPost)] =
-                make_uint4(rb + start, rb + g1, rb + g2, ((a.b0 + own) * a.cap + segs) * 64u);
+            if (posted)  // exec-masked (one scratch entry for every other lane would serialise the LDS)
+                jobtab[wave * kBinJobsPerWave + jr] = make_uint4(rb + start, rb + g1, rb + g2, ((a.b0 + own) * a.cap + segs) * 64u);
         }
 #if !LSMB_WALKFIRST
         // Key it+1's positions (VALU only), beside the flush's LDS round trips.
@@ -603,335 +606,6 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
             cnt -= m;
         }
         a.counts[(uint64_t)(a.b0 + own) * a.grid + w] = segs;
-    }
-}
-
-// Pass A with specialised waves (k_bin2, k = KMAX exact).  The stamps of
-// k_bin (LSMB_STAMP) put a C2 phase at ~5 900 cycles: the claims and slot
-// writes of 16 waves (LDS-bound, ~2 100 LDS cycles of random-address atomics
-// and stores) with the hash beside them, then a flush that is a chain of
-// dependent LDS round trips (owner fill read -> job post -> job read ->
-// segment reads -> stores) during which no wave computes, then two barrier
-// waits.  Here the workgroup's waves split the two jobs:
-//   * NH = 16 - NF hash waves own the keys (one per lane per phase, PER keys
-//     per lane in sweeps): claims, XXH3 of the next key beside them, slot
-//     writes; after the first barrier, the walk of the next key's positions
-//     (VALU only, beside the flush);
-//   * NF flush waves own the bins, BPL consecutive bins per lane (one
-//     ds_read_b128 of their fill words): after the first barrier they post
-//     every full segment of their bins into their own job table (dense: up
-//     to 16 segments per store instruction, so ~half the store instructions
-//     of a table per wave of 57 owners), write the segments with the
-//     cooperative 4-lane stores and advance their rings.
-// The same rings, fill words, regions and overflow paths as k_bin; pass B
-// and the region layout are unchanged.
-template <int NF>
-struct Bin2Geo {
-    static constexpr int NH = kBinBlock / 64 - NF;           // hash waves
-    static constexpr uint32_t KPP = NH * 64;                 // key slots per phase (per PER)
-    static constexpr uint32_t BPL = kMaxBinsPerSweep / (NF * 64);  // bins per flush lane
-    static constexpr uint32_t kJobs = 80;                    // job-table entries per flush wave (last: scratch)
-    static_assert(BPL == 4 || BPL == 8, "flush lanes read their fill words as uint4");
-};
-// LDS bytes of k_bin2: rings of nb + 1 slices, fill words for every flush-lane
-// bin (+ the sink), job tables.
-template <int NF>
-constexpr size_t bin2_lds_bytes(uint32_t nb, uint32_t ring) {
-    return ((((size_t)(nb + 1) * ring) + 3) & ~(size_t)3) * 4 + (kMaxBinsPerSweep + 4) * 4 +
-           (size_t)NF * Bin2Geo<NF>::kJobs * 16;
-}
-
-template <class Src, class W, int KMAX, bool FULL, int PER, int SL, int NF>
-__global__ __launch_bounds__(kBinBlock) void k_bin2(Src src, uint64_t n, Mod32 md, uint32_t, PassA a) {
-    using G = Bin2Geo<NF>;
-    constexpr int NH = G::NH;
-    constexpr uint32_t KPP = G::KPP, BPL = G::BPL, kJobs = G::kJobs, kPost = kJobs - 1;
-    constexpr uint32_t kMask = (1u << SL) - 1;
-    constexpr int NP = PER * KMAX;
-    extern __shared__ uint32_t sm[];
-    const uint32_t R = a.ring, R4 = 4 * a.ring, nb = a.nb;
-    uint32_t* fill = sm + ((((size_t)(nb + 1) * R) + 3) & ~(size_t)3);  // [kMaxBinsPerSweep + 4]
-    uint4* jobtab = reinterpret_cast<uint4*>(fill + kMaxBinsPerSweep + 4);
-    const uint32_t tid = threadIdx.x, w = blockIdx.x, lane = tid & 63;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: the role branches are uniform
-    for (uint32_t i = tid; i < kMaxBinsPerSweep + 4; i += kBinBlock) fill[i] = 0;
-    constexpr uint32_t kInc = 4u | (1u << 16);
-    const uint32_t sink = nb << SL;
-    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
-    const uint64_t i0 = (uint64_t)w * per, i1 = min(n, i0 + per);
-    const uint64_t iters = i1 > i0 ? (i1 - i0 + PER * KPP - 1) / (PER * KPP) : 0;  // uniform
-    const uint64_t groups = (iters + kAhead - 1) / kAhead;  // phases run in whole groups of kAhead
-    __syncthreads();
-#if LSMB_STAMP
-    uint64_t st_sum[4] = {0, 0, 0, 0}, st_prev = stamp(), st_t;
-#define LSMB_ST(q) (st_t = stamp(), st_sum[q] += st_t - st_prev, st_prev = st_t)
-#else
-#define LSMB_ST(q) ((void)0)
-#endif
-    // The two roles run separate loops with the same barriers (two per
-    // phase, the same number of phases), so each keeps only its own state in
-    // registers.
-    if (wave < (uint32_t)NH) {
-        // ------------------------------------------------ hash waves
-        const uint32_t lim = R << 16;
-        const uint32_t hl = wave * 64 + lane;
-        auto key_index = [&](uint64_t it) { return i0 + (it * KPP + hl) * PER; };
-        auto key_ok = [&](uint64_t it, int j = 0) { return it < iters && key_index(it) + j < i1; };
-        using Pre = typename Src::Pre;
-        auto fetch_keys = [&](uint64_t it, Pre (&out)[PER]) {
-#pragma unroll
-            for (int j = 0; j < PER; j++) out[j] = src.fetch(key_index(it) + j, key_ok(it, j));
-        };
-        auto walk_positions = [&](const typename Src::Seed& h, bool ok, uint32_t* out) {
-            W walk(md, h);
-#pragma unroll
-            for (int q = 0; q < KMAX; q++) {
-                const uint32_t lp = walk.pos() - (FULL ? 0u : (a.b0 << SL));
-                out[q] = (FULL || lp < sink) ? lp : sink;
-                if (q + 1 < KMAX) walk.next(md);
-            }
-            if (__builtin_expect(__ballot(!ok) != 0, 0)) {
-#pragma unroll
-                for (int q = 0; q < KMAX; q++)
-                    if (!ok) out[q] = sink;
-            }
-        };
-        uint32_t pos[NP], kinc[PER];
-        Pre pb0[PER], pb1[PER], pb2[PER], pb3[PER];
-#pragma unroll
-        for (int j = 0; j < PER; j++) {
-            const bool ok = key_ok(0, j);
-            const Pre p = src.fetch(key_index(0) + j, ok);
-            const typename Src::Seed h = ok ? src.hash_pre(p, key_index(0) + j) : typename Src::Seed{};
-            walk_positions(h, ok, pos + j * KMAX);
-            kinc[j] = ok ? kInc : 0u;
-        }
-        fetch_keys(1, pb1);
-        fetch_keys(2, pb2);
-        fetch_keys(3, pb3);
-        fetch_keys(4, pb0);
-        auto phase = [&](uint64_t it, Pre (&pre)[PER]) __attribute__((always_inline)) {
-            // claims, back to back
-            uint32_t got[NP];
-#pragma unroll
-            for (int q = 0; q < NP; q++) {
-                if (FULL)
-                    got[q] = atomicAdd(fill + (pos[q] >> SL), kinc[q / KMAX]);
-                else
-                    got[q] = pos[q] < sink ? atomicAdd(fill + (pos[q] >> SL), kInc) : 0u;
-            }
-            // XXH3 of the next key while they are in flight (pinned here)
-            typename Src::Seed nh[PER];
-            bool nok[PER];
-#pragma unroll
-            for (int j = 0; j < PER; j++) {
-                nok[j] = key_ok(it + 1, j);
-                nh[j] = src.hash_pre(pre[j], key_index(it + 1) + j);
-            }
-            fetch_keys(it + 1 + kAhead, pre);
-#pragma unroll
-            for (int j = 0; j < PER; j++) pin_seed(nh[j]);
-            // slot writes (fast path: no claim of the wave past its ring)
-            uint32_t gmax = 0;
-#pragma unroll
-            for (int q = 0; q < NP; q++) gmax = max(gmax, got[q]);
-            auto slot = [&](int q) {
-                uint32_t x = got[q] & 0xFFFFu;
-                x = min(x, x - R4);
-                return __umul24(pos[q] >> SL, R4) + x;
-            };
-            if (__builtin_expect(__ballot(gmax >= lim) == 0, 1)) {
-#pragma unroll
-                for (int q = 0; q < NP; q++)
-                    if (FULL || pos[q] < sink) *(uint32_t*)((char*)sm + slot(q)) = pos[q] & kMask;
-            } else {
-#pragma unroll
-                for (int q = 0; q < NP; q++) {
-                    if (FULL || pos[q] < sink) {
-                        if (got[q] < lim)
-                            *(uint32_t*)((char*)sm + slot(q)) = pos[q] & kMask;
-                        else if (pos[q] < sink)
-                            or_pos_global<SL>(a.gw, a.b0 + (pos[q] >> SL), pos[q] & kMask);
-                    }
-                }
-            }
-            LSMB_ST(0);
-            lds_barrier();
-            LSMB_ST(1);
-            // the next key's positions (VALU only), beside the flush waves
-#pragma unroll
-            for (int j = 0; j < PER; j++) {
-                walk_positions(nh[j], nok[j], pos + j * KMAX);
-                kinc[j] = nok[j] ? kInc : 0u;
-            }
-#pragma unroll
-            for (int q = 0; q < NP; q++) asm volatile("" ::"v"(pos[q]));
-            LSMB_ST(2);
-            lds_barrier();
-            LSMB_ST(3);
-        };
-        for (uint64_t g = 0; g < groups; g++) {
-            const uint64_t it = g * kAhead;
-            phase(it, pb1);
-            phase(it + 1, pb2);
-            phase(it + 2, pb3);
-            phase(it + 3, pb0);
-        }
-        return;
-    }
-    // ------------------------------------------------ flush waves
-    const __amdgpu_buffer_rsrc_t rgn = __builtin_amdgcn_make_buffer_rsrc(
-        region_ptr(a, 0, w), 0, (int)(a.nbins * a.cap * 64u), 0x00020000);
-    constexpr uint32_t kDrop = 0x80000000u;
-    const uint32_t fw = wave - NH, fl = fw * 64 + lane, fb0 = fl * BPL;  // this lane's bins fb0 ..
-    // A bin's ring start is not kept: its fill word holds start + 4 * claims
-    // (lo16) and claims (hi16), so start = lo16 - 4 * hi16 (mod 4R).
-    auto ring_start = [&](uint32_t f) {
-        const uint32_t s = (f & 0xFFFFu) - 4 * (f >> 16);
-        return min(s, s + R4);
-    };
-    uint32_t segs[BPL];  // region segments written, per bin
-#pragma unroll
-    for (uint32_t m = 0; m < BPL; m++) segs[m] = 0;
-    for (uint64_t ph = 0; ph < groups * kAhead; ph++) {
-        LSMB_ST(0);
-        lds_barrier();
-        LSMB_ST(1);
-        // fill words of this lane's bins (bins >= nb: the sink's and the
-        // padding's, which stay 0)
-        uint32_t fv[BPL];
-#pragma unroll
-        for (uint32_t m = 0; m < BPL; m += 4) {
-            const uint4 v = *(const uint4*)(fill + fb0 + m);
-            fv[m] = v.x, fv[m + 1] = v.y, fv[m + 2] = v.z, fv[m + 3] = v.w;
-        }
-        uint32_t cnt[BPL], start[BPL];
-        bool has[BPL], posted[BPL];
-        uint32_t base = 0;
-#pragma unroll
-        for (uint32_t m = 0; m < BPL; m++) {
-            const uint32_t b = fb0 + m;
-            start[m] = ring_start(fv[m]);
-            cnt[m] = b < nb ? min(fv[m] >> 16, R) : 0u;
-            has[m] = cnt[m] >= (uint32_t)kSegEntries;
-            const bool coop = has[m] && segs[m] < a.cap;
-            const uint64_t cm = __ballot(coop);
-            const uint32_t jr =
-                base + __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
-            posted[m] = coop && jr < kPost;
-            uint32_t g1 = start[m] + 32, g2 = start[m] + 64;
-            g1 = min(g1, g1 - R4);
-            g2 = min(g2, g2 - R4);
-            const uint32_t rb = min(b, nb) * R4;  // (padding bins: the sink's ring, in bounds)
-            jobtab[fw * kJobs + (posted[m] ? jr : kPost)] =
-                make_uint4(rb + start[m], rb + g1, rb + g2, ((a.b0 + b) * a.cap + segs[m]) * 64u);
-            base += (uint32_t)__popcll(cm);
-        }
-        const uint32_t jobs = min(base, kPost);  // wave-uniform
-        // cooperative stores: lane L writes 16 B of job r*16 + L/4
-        for (uint32_t r = 0; r * 16 < jobs; r++) {
-            const uint32_t j = r * 16 + (lane >> 2), l = lane & 3;
-            const bool valid = j < jobs;
-            const uint4 jb = jobtab[fw * kJobs + (valid ? j : kPost)];
-            const uint2 a0 = *(const uint2*)((const char*)sm + jb.x + 8 * l);
-            const uint2 a1 = *(const uint2*)((const char*)sm + jb.y + 8 * l);
-            const uint2 a2 = *(const uint2*)((const char*)sm + jb.z + 8 * l);
-            const uint2 w0 = pack3w<SL>(a0.x, a1.x, a2.x), w1 = pack3w<SL>(a0.y, a1.y, a2.y);
-            __builtin_amdgcn_raw_buffer_store_b128(u32x4{w0.x, w0.y, w1.x, w1.y}, rgn, valid ? jb.w + 16 * l : kDrop, 0,
-                                                   LSMB_STORE_AUX);
-        }
-        // advance the rings; a second segment of a bin, or an unposted one
-        // (full region / full table), per lane (rare)
-        bool rare = false;
-#pragma unroll
-        for (uint32_t m = 0; m < BPL; m++) rare |= has[m] && (!posted[m] || cnt[m] >= 2u * kSegEntries);
-        if (__builtin_expect(__ballot(rare) != 0, 0)) {
-            for (uint32_t m = 0; m < BPL; m++) {
-                if (!has[m]) continue;
-                const uint32_t b = fb0 + m;
-                const char* ring = (const char*)sm + b * R4;
-                const uint32_t nf = cnt[m] / (uint32_t)kSegEntries;
-                for (uint32_t j = 0; j < nf; j++) {
-                    if (j > 0 || !posted[m]) {  // this segment per lane
-                        uint32_t g1 = start[m] + 32, g2 = start[m] + 64;
-                        g1 = min(g1, g1 - R4);
-                        g2 = min(g2, g2 - R4);
-                        uint32_t v[kSegEntries];
-                        for (int t = 0; t < 8; t++) {
-                            v[t] = *(const uint32_t*)(ring + start[m] + 4 * t);
-                            v[t + 8] = *(const uint32_t*)(ring + g1 + 4 * t);
-                            v[t + 16] = *(const uint32_t*)(ring + g2 + 4 * t);
-                        }
-                        if (segs[m] < a.cap) {
-                            uint64_t* dst = region_ptr(a, a.b0 + b, w) + (uint64_t)segs[m] * kSegWords;
-                            for (int t = 0; t < kSegWords; t++) dst[t] = pack3<SL>(v[t], v[t + 8], v[t + 16]);
-                        } else {
-                            for (int t = 0; t < kSegEntries; t++) or_pos_global<SL>(a.gw, a.b0 + b, v[t]);
-                        }
-                    }
-                    uint32_t s2 = start[m] + 96;
-                    start[m] = min(s2, s2 - R4);
-                    segs[m] = min(segs[m] + 1, a.cap);
-                }
-                const uint32_t rem = cnt[m] - nf * (uint32_t)kSegEntries;
-                fv[m] = (start[m] + 4 * rem) | (rem << 16);
-            }
-        } else {
-#pragma unroll
-            for (uint32_t m = 0; m < BPL; m++) {
-                uint32_t s2 = start[m] + 96;
-                s2 = min(s2, s2 - R4);
-                const uint32_t rem = cnt[m] - (uint32_t)kSegEntries;
-                fv[m] = has[m] ? ((s2 + 4 * rem) | (rem << 16)) : fv[m];
-                segs[m] = has[m] ? segs[m] + 1 : segs[m];
-            }
-        }
-#pragma unroll
-        for (uint32_t m = 0; m < BPL; m += 4)
-            *(uint4*)(fill + fb0 + m) = make_uint4(fv[m], fv[m + 1], fv[m + 2], fv[m + 3]);
-        LSMB_ST(2);
-        lds_barrier();
-        LSMB_ST(3);
-    }
-#if LSMB_STAMP
-    if (lane == 0) {  // the flush waves' view of the phase
-        for (int q = 0; q < 4; q++) atomicAdd(&g_stamp[q], (unsigned long long)st_sum[q]);
-        atomicAdd(&g_stamp[4], (unsigned long long)groups * kAhead);
-        atomicAdd(&g_stamp[5], 1ull);
-    }
-#endif
-#undef LSMB_ST
-    // leftovers: each bin's open segment (padded with its first entry), then
-    // the region's segment count
-#pragma unroll
-    for (uint32_t m = 0; m < BPL; m++) {
-        const uint32_t b = fb0 + m;
-        if (b >= nb) continue;
-        const uint32_t fvb = fill[b];
-        uint32_t cnt = min(fvb >> 16, R), start = ring_start(fvb);
-        const char* ring = (const char*)sm + b * R4;
-        while (cnt) {
-            const uint32_t mm = min(cnt, (uint32_t)kSegEntries);
-            uint32_t v[kSegEntries];
-#pragma unroll
-            for (int t = 0; t < kSegEntries; t++) {
-                uint32_t x = start + 4 * ((uint32_t)t < mm ? t : 0);
-                x = min(x, x - R4);
-                v[t] = *(const uint32_t*)(ring + x);
-            }
-            if (segs[m] < a.cap) {
-                uint64_t* dst = region_ptr(a, a.b0 + b, w) + (uint64_t)segs[m] * kSegWords;
-#pragma unroll
-                for (int t = 0; t < kSegWords; t++) dst[t] = pack3<SL>(v[t], v[t + 8], v[t + 16]);
-                segs[m]++;
-            } else {
-                for (uint32_t t = 0; t < mm; t++) or_pos_global<SL>(a.gw, a.b0 + b, v[t]);
-            }
-            uint32_t x = start + 4 * mm;
-            start = min(x, x - R4);
-            cnt -= mm;
-        }
-        a.counts[(uint64_t)(a.b0 + b) * a.grid + w] = segs[m];
     }
 }
 
@@ -1202,36 +876,9 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
                 kern<<<dim3(pl.grid), dim3(kBinBlock), smem, st>>>(src, n, md, k, a);
             };
             const bool full = pl.sweeps == 1;
-            // k_bin2 (specialised hash / flush waves) where its LDS fits;
-            // LSMB_BIN2=0 selects k_bin (measurement knob)
-            static const int bin2_env = [] {
-                const char* e = getenv("LSMB_BIN2");
-                return e ? atoi(e) : 1;
-            }();
-            constexpr int NF = 4;
-            const size_t smem2 = bin2_lds_bytes<NF>(a.nb, a.ring);
-            const bool use2 = bin2_env != 0 && smem2 <= kLdsBytes;
-            auto go2 = [&](auto kern) {
-                set_max_lds((const void*)kern);
-                kern<<<dim3(pl.grid), dim3(kBinBlock), smem2, st>>>(src, n, md, k, a);
-            };
             auto go7 = [&](auto slc) {  // k = 7 (BloomFilter::new at fpr 0.01), bin width 2^SL
                 constexpr int SL = decltype(slc)::value;
                 const bool two = pl.keys_per_lane == 2;
-                if (use2) {
-                    if (w32) {
-                        if (full && two) go2(k_bin2<Src, Walk32, 7, true, 2, SL, NF>);
-                        else if (full) go2(k_bin2<Src, Walk32, 7, true, 1, SL, NF>);
-                        else if (two) go2(k_bin2<Src, Walk32, 7, false, 2, SL, NF>);
-                        else go2(k_bin2<Src, Walk32, 7, false, 1, SL, NF>);
-                    } else {
-                        if (full && two) go2(k_bin2<Src, Walk64, 7, true, 2, SL, NF>);
-                        else if (full) go2(k_bin2<Src, Walk64, 7, true, 1, SL, NF>);
-                        else if (two) go2(k_bin2<Src, Walk64, 7, false, 2, SL, NF>);
-                        else go2(k_bin2<Src, Walk64, 7, false, 1, SL, NF>);
-                    }
-                    return;
-                }
                 if (w32) {
                     if (full && two) go(k_bin<Src, Walk32, 7, true, true, 2, SL>);
                     else if (full) go(k_bin<Src, Walk32, 7, true, true, 1, SL>);
