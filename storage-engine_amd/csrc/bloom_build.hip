@@ -56,9 +56,6 @@
 #ifndef LSMB_STAMP
 #define LSMB_STAMP 0
 #endif
-#ifndef LSMB_WALKFIRST
-#define LSMB_WALKFIRST 0  // measurement variant: the walk pinned between the fill read and its use
-#endif
 
 namespace lsmb {
 namespace {
@@ -248,9 +245,6 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
     uint4* jobtab = reinterpret_cast<uint4*>(sm + ((((size_t)(nb + 1) * (R + 1)) + 3) & ~(size_t)3));
     const uint32_t tid = threadIdx.x, w = blockIdx.x, lane = tid & 63, wave = tid >> 6;
     for (uint32_t i = tid; i <= nb; i += kBinBlock) fill[i] = 0;
-    // each wave's scratch job entry (read by the store rounds' idle lanes):
-    // in-bounds ring addresses, a dropped store offset
-    if (lane == 0) jobtab[wave * kBinJobsPerWave + kBinJobsPerWave - 1] = make_uint4(0, 0, 0, 0x80000000u);
     // Workgroup w's regions as a raw buffer: a store at an offset past
     // num_records is dropped by the hardware, which lets every lane issue the
     // flush stores unconditionally (see the flush).
@@ -321,13 +315,11 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
 #if LSMB_STAMP
     uint64_t st_sum[4] = {0, 0, 0, 0}, st_prev = stamp(), st_t;
 #endif
-    // One phase: claim key it's positions; hash key it+1 (from `pre`) and
-    // reload `pre` with key it+1+kAhead while the claims are in flight; store
-    // the entries; barrier; flush, with key it+1's position walk computed
-    // beside it; barrier.  The phase's VALU work is split over both barrier
-    // sections so neither is all-LDS (the claims, slot writes and flush) or
-    // all-VALU: stamps of the earlier form (hash and walk both before the
-    // first barrier) showed the flush section VALU-idle for ~29 % of a phase.
+    // One phase: claim key it's positions, hash and walk key it+1 (from
+    // `pre`) and reload `pre` with key it+1+kAhead, store the entries,
+    // barrier, flush, barrier.  (Moving the walk past the first barrier, next
+    // to the flush's LDS round trips, measured neutral at C2 and 0.15 ms
+    // slower on C5's sweeps: DESIGN.md section 4.2.)
     auto phase = [&](uint64_t it, Pre (&pre)[PER]) __attribute__((always_inline)) {
         // Claims for this phase's keys, back to back.
         uint32_t got[NP];
@@ -345,19 +337,22 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
                 }
             }
         }
-        // While the claims are in flight: XXH3 of key it+1, pinned here (an
-        // empty asm consuming it), else the compiler sinks it past the
-        // barrier, where the claims' round trip is then exposed.
-        typename Src::Seed nh[PER];
-        bool nok[PER];
+        // While the claims are in flight: hash and walk key it+1, pinned here
+        // (an empty asm that consumes the positions): otherwise the compiler
+        // sinks the whole hash + walk below the barrier, where every wave
+        // computes while none has LDS work, and the claims' round trip is
+        // exposed instead.
+        uint32_t npos[NP], nkinc[PER];
 #pragma unroll
         for (int j = 0; j < PER; j++) {
-            nok[j] = key_ok(it + 1, j);
-            nh[j] = src.hash_pre(pre[j], key_index(it + 1) + j);
+            const bool ok = key_ok(it + 1, j);
+            walk_positions(src.hash_pre(pre[j], key_index(it + 1) + j), ok, npos + j * KMAX);
+            nkinc[j] = ok ? kInc : 0u;
         }
         fetch_keys(it + 1 + kAhead, pre);
 #pragma unroll
-        for (int j = 0; j < PER; j++) pin_seed(nh[j]);
+        for (int q = 0; q < NP; q++)
+            if (EXACT || (uint32_t)q < k) asm volatile("" ::"v"(npos[q]));
         // Store the claimed entries.  Fast path (every claim of the wave fits
         // its ring): slot address = b * R4 + wrapped ring offset, one full-rate
         // 24-bit multiply-add, no per-position select.  A wave with an
@@ -397,6 +392,10 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
                 }
             }
         }
+#pragma unroll
+        for (int q = 0; q < NP; q++) pos[q] = npos[q];
+#pragma unroll
+        for (int j = 0; j < PER; j++) kinc[j] = nkinc[j];
 #if LSMB_STAMP
         st_t = stamp(), st_sum[0] += st_t - st_prev, st_prev = st_t;
 #endif
@@ -414,28 +413,16 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
         // so the flush issues exactly kCoopRounds stores per wave per phase,
         // at a dropped offset where a lane has nothing to write — a static
         // store count also keeps the compiler's vmcnt waits for the
-        // prefetched keys exact.  The common case is branch-free (every lane
-        // reads a fill word — non-owners the sink's — and writes a job entry,
-        // the non-posting ones into the table's last, scratch entry), so the
-        // walk below can fill the flush's LDS round trips; a second segment
-        // of the same slice, or a full region, takes the per-lane path (rare).
-        const uint32_t ownc = owner ? own : nb;  // non-owners: the sink's fill word (stays 0)
-        uint32_t fv = fill[ownc];
-#if LSMB_WALKFIRST
-        // Key it+1's positions (VALU only) while the fill word is read.
-        uint32_t npos[NP], nkinc[PER];
-#pragma unroll
-        for (int j = 0; j < PER; j++) {
-            walk_positions(nh[j], nok[j], npos + j * KMAX);
-            nkinc[j] = nok[j] ? kInc : 0u;
+        // prefetched keys exact.  A second segment of the same slice, or a
+        // region already full, takes the per-lane path below (rare).
+        uint32_t cnt = 0;
+        if (owner) {
+            cnt = min(fill[own] >> 16, R);
+            if (LSMB_ABL & 1) {
+                fill[own] = start;
+                cnt = 0;
+            }
         }
-#pragma unroll
-        for (int q = 0; q < NP; q++)
-            if (EXACT || (uint32_t)q < k) asm volatile("" ::"v"(npos[q]));
-        asm volatile("" : "+v"(fv));
-#endif
-        uint32_t cnt = owner ? min(fv >> 16, R) : 0u;
-        if (LSMB_ABL & 1) cnt = 0;
         const bool has = cnt >= (uint32_t)kSegEntries;
         const char* ring = (const char*)sm + own * R4;
         uint4 x0, x1, y0, y1, z0, z1;
@@ -470,55 +457,45 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
 #endif
         };
         // 1. post jobs (owner lanes with a full segment and room in the region)
-        constexpr uint32_t kPost = kBinJobsPerWave - 1;  // the last entry is scratch
         const bool coop = has && segs < a.cap;
         const uint64_t cm = __ballot(coop);
-        const uint32_t jobs = min((uint32_t)__popcll(cm), kPost);  // wave-uniform
-        const uint32_t jr = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
-        const bool posted = coop && jr < kPost;
-        {
-            const uint32_t rb = ownc * R4;
-            uint32_t g1 = start + 32, g2 = start + 64;
-            g1 = min(g1, g1 - R4);
-            g2 = min(g2, g2 - R4);
-            if (posted)  // exec-masked (one scratch entry for every other lane would serialise the LDS)
-                jobtab[wave * kBinJobsPerWave + jr] = make_uint4(rb + start, rb + g1, rb + g2, ((a.b0 + own) * a.cap + segs) * 64u);
+        const uint32_t jobs = min((uint32_t)__popcll(cm), kBinJobsPerWave);  // wave-uniform
+        bool posted = false;
+        if (coop) {
+            const uint32_t j = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
+            if (j < kBinJobsPerWave) {
+                const uint32_t rb = own * R4;
+                uint32_t g1 = start + 32, g2 = start + 64;
+                g1 = min(g1, g1 - R4);
+                g2 = min(g2, g2 - R4);
+                jobtab[wave * kBinJobsPerWave + j] =
+                    make_uint4(rb + start, rb + g1, rb + g2, ((a.b0 + own) * a.cap + segs) * 64u);
+                posted = true;
+            }
         }
-#if !LSMB_WALKFIRST
-        // Key it+1's positions (VALU only), beside the flush's LDS round trips.
-        uint32_t npos[NP], nkinc[PER];
-#pragma unroll
-        for (int j = 0; j < PER; j++) {
-            walk_positions(nh[j], nok[j], npos + j * KMAX);
-            nkinc[j] = nok[j] ? kInc : 0u;
-        }
-#endif
+        // (the job table is this wave's own: its LDS writes and reads stay in order)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         // 2. kCoopRounds store instructions: lane L writes 16 B of job r*16 + L/4
-        constexpr uint32_t kCoopRounds = (kPost + 15) / 16;
+        constexpr uint32_t kCoopRounds = (kBinJobsPerWave + 15) / 16;
 #pragma unroll
         for (uint32_t r = 0; r < kCoopRounds; r++) {
             const uint32_t j = r * 16 + (lane >> 2), l = lane & 3;
-            const bool valid = j < jobs;
-            const uint4 jb = jobtab[wave * kBinJobsPerWave + (valid ? j : kPost)];
-            // segment word 2l+e = pack3<SL>(group0[2l+e], group1[2l+e], group2[2l+e])
-            const uint2 a0 = *(const uint2*)((const char*)sm + jb.x + 8 * l);
-            const uint2 a1 = *(const uint2*)((const char*)sm + jb.y + 8 * l);
-            const uint2 a2 = *(const uint2*)((const char*)sm + jb.z + 8 * l);
-            const uint2 w0 = pack3w<SL>(a0.x, a1.x, a2.x), w1 = pack3w<SL>(a0.y, a1.y, a2.y);
-            const uint32_t off = (valid && !(LSMB_ABL & 16)) ? jb.w + 16 * l : kDrop;
+            uint32_t off = kDrop;
+            uint2 w0 = make_uint2(0, 0), w1 = make_uint2(0, 0);
+            if (j < jobs) {
+                const uint4 jb = jobtab[wave * kBinJobsPerWave + j];
+                // segment word 2l+e = pack3<SL>(group0[2l+e], group1[2l+e], group2[2l+e])
+                const uint2 a0 = *(const uint2*)((const char*)sm + jb.x + 8 * l);
+                const uint2 a1 = *(const uint2*)((const char*)sm + jb.y + 8 * l);
+                const uint2 a2 = *(const uint2*)((const char*)sm + jb.z + 8 * l);
+                w0 = pack3w<SL>(a0.x, a1.x, a2.x);
+                w1 = pack3w<SL>(a0.y, a1.y, a2.y);
+                off = (LSMB_ABL & 16) ? kDrop : jb.w + 16 * l;
+            }
             if (!(LSMB_ABL & 8)) __builtin_amdgcn_raw_buffer_store_b128(u32x4{w0.x, w0.y, w1.x, w1.y}, rgn, off, 0, LSMB_STORE_AUX);
         }
-        // 3. owners advance past the posted segment; the rest per lane (rare)
-        const bool rare = has && (!posted || cnt >= 2u * kSegEntries);
-        if (__builtin_expect(__ballot(rare) == 0, 1)) {
-            uint32_t s2 = start + 96;
-            s2 = min(s2, s2 - R4);
-            const uint32_t rem = cnt - (uint32_t)kSegEntries;
-            const uint32_t nf = has ? ((s2 + 4 * rem) | (rem << 16)) : ((LSMB_ABL & 1) && owner ? start : fv);
-            start = has ? s2 : start;
-            segs = has ? segs + 1 : segs;
-            fill[ownc] = nf;  // unchanged where nothing was flushed (non-owners: the sink's 0)
-        } else if (has) {
+        // 3. owners advance past the posted segment; the rest per lane
+        if (has) {
             if (!posted) {
                 read_segment();
                 if (segs < a.cap)
@@ -543,16 +520,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
             }
             const uint32_t rem = cnt - nf * (uint32_t)kSegEntries;
             fill[own] = (start + 4 * rem) | (rem << 16);
-        } else if ((LSMB_ABL & 1) && owner) {
-            fill[own] = start;
         }
-#pragma unroll
-        for (int q = 0; q < NP; q++) {
-            if (EXACT || (uint32_t)q < k) asm volatile("" ::"v"(npos[q]));
-            pos[q] = npos[q];
-        }
-#pragma unroll
-        for (int j = 0; j < PER; j++) kinc[j] = nkinc[j];
 #if LSMB_STAMP
         st_t = stamp(), st_sum[2] += st_t - st_prev, st_prev = st_t;
 #endif
