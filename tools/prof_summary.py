@@ -79,15 +79,20 @@ def main(d):
                 print("- %s: %s = %.4g -> %.1f MB%s" % (kn, sub.split("_")[0].upper() + "_SIZE", m, mb,
                                                        " (x2, gfx950)" if sub.startswith("fetch") else ""))
         print()
+    pmc(d, ("fetch", "write", "sq1", "sq2"), "PMC counters, C2 bench (mean per dispatch)")
+    pmc(d, ("sq1_c5", "sq2_c5"), "PMC counters, C5 shard (mean per dispatch)")
+
+
+def pmc(d, subs, title):
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
-    for sub in ("fetch", "write", "sq1", "sq2"):
+    for sub in subs:
         p = os.path.join(d, sub, "run_counter_collection.csv")
         if not os.path.exists(p):
             continue
         for r in csv.DictReader(open(p)):
             agg[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
     if agg:
-        print("## PMC counters (mean per dispatch)\n")
+        print("## %s\n" % title)
         for kn, cs in sorted(agg.items()):
             if not any(x in kn for x in ("k_", "lsmb")):
                 continue

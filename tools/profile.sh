@@ -24,6 +24,10 @@ C5="$REPO/bench.py --global-keys 125000000 --filter-keys 1000000000 --steps 4 --
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats_c5" -o run -- python3 $C5 > "$OUT/stats_c5.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch_c5" -o run -- python3 $C5 > "$OUT/fetch_c5.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write_c5" -o run -- python3 $C5 > "$OUT/write_c5.log" 2>&1
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_WAIT_INST_LDS \
+    --output-format csv -d "$OUT/sq1_c5" -o run -- python3 $C5 > "$OUT/sq1_c5.log" 2>&1
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_BUSY_CYCLES \
+    --output-format csv -d "$OUT/sq2_c5" -o run -- python3 $C5 > "$OUT/sq2_c5.log" 2>&1
 # C4 var-len build kernels (k_bin<ks::VarLen...>, k_apply), kernel trace only
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats_c4" -o run -- \
     python3 $REPO/bench.py --steps 6 --warmup 2 --no-cpu-baseline --no-e2e --no-probe --no-exact10 --keys-per-gpu 1000000 \
