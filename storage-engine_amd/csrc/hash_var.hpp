@@ -86,6 +86,25 @@ void k_hash_var(const uint8_t* __restrict__ d, const uint64_t* __restrict__ o, u
     const uint32_t t = threadIdx.x;
     const uint64_t i0 = (uint64_t)blockIdx.x * KEYS;
     const uint32_t m = (uint32_t)min<uint64_t>(KEYS, n - i0);
+    // The first window's loads go out before anything else, as LDS-DMA (no
+    // VGPRs held across the lane sort): the window and the offsets then share
+    // one memory round trip instead of two back to back (C4: k_hash_var +
+    // pass A 4.27 -> 4.13 ms).  A persistent form that keeps the next block's
+    // window in flight in a second window while hashing (two workgroups per
+    // CU) took 5.76 ms: the hash needs the four workgroups' waves.
+    {
+        const uintptr_t A0 = (uintptr_t)(d + o[i0]) & ~(uintptr_t)15;
+        const uint32_t nb0 = (uint32_t)(min(A0 + (uintptr_t)WIN, (uintptr_t)(d + o[i0 + m])) - A0);
+        const uint32_t wv = t >> 6;
+#pragma unroll
+        for (uint32_t r = 0; r < kPieces; r++) {
+            const uint32_t q = (r * KEYS + t) * 16;
+            if (q < nb0)
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(A0 + q),
+                                                 (__attribute__((address_space(3))) void*)(win + (r * KEYS + wv * 64) * 4),
+                                                 16, 0, 0);
+        }
+    }
     // lane assignment by length class (a counting sort of the block's keys)
     uint32_t cls = 15;
     if (t < m) cls = MODE == 2 ? 0 : len_class(o[i0 + t + 1] - o[i0 + t]);  // MODE 2 (microbenchmark): no sort
@@ -114,16 +133,18 @@ void k_hash_var(const uint8_t* __restrict__ d, const uint64_t* __restrict__ o, u
         const uintptr_t A = (uintptr_t)(d + o[i0 + f]) & ~(uintptr_t)15;
         const uintptr_t wend = min(A + (uintptr_t)WIN, end);
         const uint32_t nb = (uint32_t)(wend - A);
-        uint4 v[kPieces];
+        if (f > 0) {  // (round 0's window is already in LDS)
+            uint4 v[kPieces];
 #pragma unroll
-        for (uint32_t r = 0; r < kPieces; r++) {
-            const uint32_t q = (r * KEYS + t) * 16;
-            v[r] = q < nb ? ld_stream16((const uint4*)(A + q)) : make_uint4(0, 0, 0, 0);
-        }
+            for (uint32_t r = 0; r < kPieces; r++) {
+                const uint32_t q = (r * KEYS + t) * 16;
+                v[r] = q < nb ? ld_stream16((const uint4*)(A + q)) : make_uint4(0, 0, 0, 0);
+            }
 #pragma unroll
-        for (uint32_t r = 0; r < kPieces; r++) {
-            const uint32_t q = (r * KEYS + t) * 16;
-            if (q < nb) *(uint4*)((char*)win + q) = v[r];
+            for (uint32_t r = 0; r < kPieces; r++) {
+                const uint32_t q = (r * KEYS + t) * 16;
+                if (q < nb) *(uint4*)((char*)win + q) = v[r];
+            }
         }
         __syncthreads();
         // keys f.. that end inside the window: a prefix (offsets ascend)

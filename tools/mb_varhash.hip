@@ -75,22 +75,22 @@ int main(int argc, char** argv) {
         k_fill<<<4096, 256>>>((uint64_t*)d, bytes / 8);
         CK(hipMemcpy(o, off.data(), (n + 1) * 8, hipMemcpyHostToDevice));
         const uint32_t g = (uint32_t)((n + 255) / 256);
-        const float t_stage = timeit([&] { k_hash_var<1><<<g, 256>>>(d, o, n, out); });
-        const float t_lds = timeit([&] { k_hash_var<0><<<g, 256>>>(d, o, n, out); });
-        const float t_dir = timeit([&] { k_hash_direct<<<g, 256>>>(d, o, n, out); });
+        const float t_stage = timeit([&] { k_hash_var<1><<<g, 256>>>(d, o, n, OutH128(out)); });
+        const float t_lds = timeit([&] { k_hash_var<0><<<g, 256>>>(d, o, n, OutH128(out)); });
+        const float t_dir = timeit([&] { k_hash_direct<<<g, 256>>>(d, o, n, OutH128(out)); });
         const uint32_t g2 = (uint32_t)((n + 127) / 128);
-        const float t_128_20 = timeit([&] { k_hash_var<0, 128, 20480><<<g2, 128>>>(d, o, n, out); });
-        const float t_128_24 = timeit([&] { k_hash_var<0, 128, 24576><<<g2, 128>>>(d, o, n, out); });
-        const float t_256_32 = timeit([&] { k_hash_var<0, 256, 32768><<<g, 256>>>(d, o, n, out); });
+        const float t_128_20 = timeit([&] { k_hash_var<0, 128, 20480><<<g2, 128>>>(d, o, n, OutH128(out)); });
+        const float t_128_24 = timeit([&] { k_hash_var<0, 128, 24576><<<g2, 128>>>(d, o, n, OutH128(out)); });
+        const float t_256_32 = timeit([&] { k_hash_var<0, 256, 32768><<<g, 256>>>(d, o, n, OutH128(out)); });
         const uint32_t g3 = (uint32_t)((n + 63) / 64);
-        const float t_64_12 = timeit([&] { k_hash_var<0, 64, 12288><<<g3, 64>>>(d, o, n, out); });
-        const float t_nosort = timeit([&] { k_hash_var<2><<<g, 256>>>(d, o, n, out); });
-        const float tB = timeit([&] { k_hash_var<0, 256, 36864, 4><<<g, 256>>>(d, o, n, out); });
-        const float tC = timeit([&] { k_hash_var<0, 256, 40960, 3><<<g, 256>>>(d, o, n, out); });
+        const float t_64_12 = timeit([&] { k_hash_var<0, 64, 12288><<<g3, 64>>>(d, o, n, OutH128(out)); });
+        const float t_nosort = timeit([&] { k_hash_var<2><<<g, 256>>>(d, o, n, OutH128(out)); });
+        const float tB = timeit([&] { k_hash_var<0, 256, 36864, 4><<<g, 256>>>(d, o, n, OutH128(out)); });
+        const float tC = timeit([&] { k_hash_var<0, 256, 40960, 3><<<g, 256>>>(d, o, n, OutH128(out)); });
         const uint32_t g192 = (uint32_t)((n + 191) / 192);
-        const float tD = timeit([&] { k_hash_var<0, 192, 36864, 4><<<g192, 192>>>(d, o, n, out); });
-        const float tE = timeit([&] { k_hash_var<0, 128, 18432, 4><<<g2, 128>>>(d, o, n, out); });
-        const float tF = timeit([&] { k_hash_var<0, 256, 36864, 0><<<g, 256>>>(d, o, n, out); });
+        const float tD = timeit([&] { k_hash_var<0, 192, 36864, 4><<<g192, 192>>>(d, o, n, OutH128(out)); });
+        const float tE = timeit([&] { k_hash_var<0, 128, 18432, 4><<<g2, 128>>>(d, o, n, OutH128(out)); });
+        const float tF = timeit([&] { k_hash_var<0, 256, 36864, 0><<<g, 256>>>(d, o, n, OutH128(out)); });
         printf("   no class sort %.3f | 256/36K/w4 %.3f  256/40K/w3 %.3f  192/36K/w4 %.3f  128/18K/w4 %.3f  256/36K %.3f ms\n",
                t_nosort, tB, tC, tD, tE, tF);
         // k_hash_var (LDS window) vs per-lane global reads: identical records
