@@ -77,7 +77,7 @@ int main(int argc, char** argv) {
         const uint32_t g = (uint32_t)((n + 255) / 256);
         const float t_stage = timeit([&] { k_hash_var<1><<<g, 256>>>(d, o, n, OutH128(out)); });
         const float t_lds = timeit([&] { k_hash_var<0><<<g, 256>>>(d, o, n, OutH128(out)); });
-        const float t_dir = timeit([&] { k_hash_direct<<<g, 256>>>(d, o, n, OutH128(out)); });
+        const float t_dir = timeit([&] { k_hash_direct<<<g, 256>>>(d, o, n, out); });
         const uint32_t g2 = (uint32_t)((n + 127) / 128);
         const float t_128_20 = timeit([&] { k_hash_var<0, 128, 20480><<<g2, 128>>>(d, o, n, OutH128(out)); });
         const float t_128_24 = timeit([&] { k_hash_var<0, 128, 24576><<<g2, 128>>>(d, o, n, OutH128(out)); });
@@ -95,7 +95,7 @@ int main(int argc, char** argv) {
                t_nosort, tB, tC, tD, tE, tF);
         // k_hash_var (LDS window) vs per-lane global reads: identical records
         std::vector<uint4> ha(n), hb(n);
-        k_hash_var<0><<<g, 256>>>(d, o, n, out);
+        k_hash_var<0><<<g, 256>>>(d, o, n, OutH128(out));
         CK(hipMemcpy(ha.data(), out, n * 16, hipMemcpyDeviceToHost));
         k_hash_direct<<<g, 256>>>(d, o, n, out);
         CK(hipMemcpy(hb.data(), out, n * 16, hipMemcpyDeviceToHost));
