@@ -136,26 +136,33 @@ struct Walk32T {
 using Walk32 = Walk32T<Mod32>;
 using Walk14 = Walk32T<Mod14>;  // d < 2^14 (Mod14's reduction)
 
-// The same walk for any d < 2^32 (64-bit intermediate sums).
+// The same walk for any d < 2^32.  r + s < 2d can exceed 2^32 when d > 2^31:
+// the 32-bit add's carry-out stands for the 33rd bit, so one conditional
+// subtraction still finishes the step (no 64-bit sums: C5's 2^32-1-bit
+// filter walks as cheaply as Walk32).
+LSMB_HD uint32_t add_mod_wide(uint32_t a, uint32_t b, uint32_t d) {  // (a + b) mod d, a, b < d
+    uint32_t u;
+    const bool c = __builtin_add_overflow(a, b, &u);
+    return (c || u >= d) ? u - d : u;
+}
+
 struct Walk64 {
     using Mod = Mod32;
     uint64_t x, h2;
-    uint32_t r, s;
+    uint32_t r, s0, s1, d;
 
-    LSMB_HD Walk64(const Mod32& md, uint64_t h1, uint64_t h2_) : x(h1), h2(h2_) {
+    LSMB_HD Walk64(const Mod32& md, uint64_t h1, uint64_t h2_) : x(h1), h2(h2_), d(md.d) {
         r = md.reduce(h1);
-        s = md.reduce(h2_);
+        s0 = md.reduce(h2_);
+        s1 = md.dt == md.d ? s0 : add_mod_wide(s0, md.dt, md.d);  // (s0 + 2^64 - t64) mod d
     }
     LSMB_HD Walk64(const Mod32& md, const H128& h) : Walk64(md, h.lo, h.hi) {}
     LSMB_HD uint32_t pos() const { return r; }
-    LSMB_HD void next(const Mod32& md) {
+    LSMB_HD void next(const Mod32&) {
         uint64_t nx;
         const bool carry = __builtin_add_overflow(x, h2, &nx);
         x = nx;
-        uint64_t u = (uint64_t)r + s;
-        if (u >= md.d) u -= md.d;
-        if (carry) u = (u >= md.t64) ? u - md.t64 : u + md.dt;
-        r = (uint32_t)u;
+        r = add_mod_wide(r, carry ? s1 : s0, d);
     }
 };
 
@@ -203,15 +210,14 @@ struct RecWalk32 {  // d <= 2^31, as Walk32
 
 struct RecWalk64 {  // any d < 2^32, as Walk64
     using Mod = Mod32;
-    uint32_t r, s, c;
-    LSMB_HD RecWalk64(const Mod32&, const WalkRec& q) : r(q.r), s(q.s), c(q.c) {}
+    uint32_t r, s0, s1, c, d;
+    LSMB_HD RecWalk64(const Mod32& md, const WalkRec& q) : r(q.r), s0(q.s), c(q.c), d(md.d) {
+        s1 = md.dt == md.d ? s0 : add_mod_wide(s0, md.dt, md.d);
+    }
     LSMB_HD uint32_t pos() const { return r; }
-    LSMB_HD void next(const Mod32& md) {
-        uint64_t u = (uint64_t)r + s;
-        if (u >= md.d) u -= md.d;
-        if (c & 1u) u = (u >= md.t64) ? u - md.t64 : u + md.dt;
+    LSMB_HD void next(const Mod32&) {
+        r = add_mod_wide(r, (c & 1u) ? s1 : s0, d);
         c >>= 1;
-        r = (uint32_t)u;
     }
 };
 
