@@ -959,15 +959,18 @@ PartitionPlan plan_partition_sl(uint32_t num_bits, uint32_t k, uint64_t n, int n
             break;
         }
     }
-    // k = 7 sweeps take two keys per lane per phase when the ring still
-    // holds a phase's doubled arrivals (C5 shard: pass A 2.64 -> 2.59 ms).
-    // Single-sweep filters keep one even where the rings would hold two:
-    // it is slower there (4.97e8 bits, 100 M keys: 0.995 -> 1.026 ms).
-    // LSMB_SWEEP_PER=1 / =2 forces one / two (measurement knob).
+    // k = 7 sweeps take two keys per lane per phase when the ring holds a
+    // phase's doubled arrivals to within one 8-entry group: C5's 32-entry
+    // rings (2^21-bit bins, 1024 per sweep; need2 = 40) then send ~0.45 % of
+    // the positions to the exact global-atomic path, and pass A still gains
+    // (C5 shard: 2.38 -> 2.33 ms).  Single-sweep filters keep one even where
+    // the rings would hold two: it is slower there (4.97e8 bits, 100 M keys:
+    // 0.995 -> 1.026 ms).  LSMB_SWEEP_PER=1 / =2 forces one / two
+    // (measurement knob).
     if (k == 7) {
         const char* e = getenv("LSMB_SWEEP_PER");
         const uint32_t need2 = (kSegEntries + (uint32_t)ceil(2 * lambda + 2.0 * sqrt(2 * lambda)) + 7) & ~7u;
-        if ((pl.sweeps > 1 && pl.ring >= need2 && !(e && atoi(e) == 1)) || (e && atoi(e) == 2)) pl.keys_per_lane = 2;
+        if ((pl.sweeps > 1 && pl.ring + 8 >= need2 && !(e && atoi(e) == 1)) || (e && atoi(e) == 2)) pl.keys_per_lane = 2;
     }
     // 1024-thread workgroups (one resident per CU), at least ~kBinBlock keys
     // each: two per CU for 2^20-bit bins — pass B then streams twice as many,
