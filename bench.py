@@ -47,12 +47,15 @@ def parse():
     ap.add_argument("--probe-keys", type=int, default=10_000_000)
     ap.add_argument("--probe-filters", type=int, default=8)
     ap.add_argument("--no-probe", action="store_true")
+    ap.add_argument("--accumulate", action="store_true",
+                    help="time zero + the OR-accumulate build (lsmb_build_fixed_dev) instead of the fresh build")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time box")
     ap.add_argument("--verify", action="store_true", help="check the built filter against the oracle")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory end-to-end measurement")
     ap.add_argument("--no-varlen", action="store_true", help="skip the C4 variable-length build leg")
     ap.add_argument("--no-exact10", action="store_true", help="skip the C2 exact 10 bits/key leg")
+    ap.add_argument("--no-c1", action="store_true", help="skip the C1-on-the-GPU leg")
     ap.add_argument("--no-overlap", action="store_true",
                     help="N > 1: build the whole filter, then OR-allreduce it (no per-sweep overlap)")
     ap.add_argument("--varlen-keys", type=int, default=100_000_000)
@@ -284,9 +287,15 @@ def main():
     words = torch.zeros(nw, dtype=torch.int64, device=dev)
     host_coll = world > 1 and args.backend != "nccl"
 
+    # BloomFilterBuilder::{new, add_key, build} (src/bloom/builder.rs:14-28):
+    # lsmb_build_fixed_dev_new writes every word of the filter (output-only
+    # words: no zeroing pass, pass B never reads the old words).
     def build():
-        words.zero_()
-        ctx.build_fixed_dev(keys, 16, npg, nb, k, words)
+        if args.accumulate:  # measurement: the OR-accumulate entry point after a zeroing pass
+            words.zero_()
+            ctx.build_fixed_dev(keys, 16, npg, nb, k, words)
+        else:
+            ctx.build_fixed_dev_new(keys, 16, npg, nb, k, words)
 
     def allreduce():
         if world > 1:
@@ -306,10 +315,9 @@ def main():
             build()
             allreduce()
             return
-        words.zero_()
         main = torch.cuda.current_stream(dev)
         for s, (a, b) in enumerate(ranges):
-            ctx.build_fixed_dev_sweep(keys, 16, npg, nb, k, words, s)
+            ctx.build_fixed_dev_sweep_new(keys, 16, npg, nb, k, words, s)
             sweep_ev[s].record(main)
             side.wait_event(sweep_ev[s])
             with torch.cuda.stream(side):
@@ -405,6 +413,9 @@ def main():
                                   % (cfg_name, args.filter_keys or total, total, nmax),
                       "keys_per_gpu": nmax, "global_keys": total, "num_bits": nb, "k": k,
                       "filter_bytes": 8 * nw, "strategy": strategy, "scaling": scaling,
+                      "entry_point": "lsmb_build_fixed_dev_new (BloomFilter::new + insert per key; "
+                                     "output-only words, every word written once)" if world == 1 else
+                                     "lsmb_build_fixed_dev_sweep_new per sweep + OR-allreduce",
                       "parallelism": "dp%d" % world}}
     if args.filter_keys:
         out["config"]["filter_sized_for_keys"] = args.filter_keys
@@ -413,7 +424,7 @@ def main():
         moved = 2 * (world - 1) / world * 8 * nw
         out["config"]["backend"] = args.backend
         out["step_split"] = {"build_ms": round(build_ms, 4), "or_allreduce_ms": round(coll_ms, 4),
-                             "what": "serial steps (untimed pass), slowest rank: zero + device build / "
+                             "what": "serial steps (untimed pass), slowest rank: device build (fresh) / "
                                      "bitwise-OR allreduce (all_to_all reduce-scatter + native OR kernel "
                                      "+ all_gather) of the whole filter",
                              "serial_ms_per_step": round(serial_ms, 4),
@@ -472,7 +483,7 @@ def main():
         out["probe"] = bench_probe(ctx, dev, args, world, rank, max_over_ranks)
     if world == 1 and not args.no_exact10:
         out["c2_exact_10_bits_per_key"] = bench_exact10(ctx, keys, npg)
-    if world == 1:
+    if world == 1 and not args.no_c1:
         out["c1_gpu"] = bench_c1_gpu(ctx, dev)
     if not args.no_e2e and rank == 0 and world == 1:
         out["e2e"] = bench_e2e(ctx, keys, npg, nb, k)
@@ -524,14 +535,12 @@ def bench_c1_gpu(ctx, dev, reps=20):
     out = torch.zeros((2 * n, 1), dtype=torch.uint8, device=dev)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     for _ in range(3):
-        w.zero_()
-        ctx.build_fixed_dev(mem, 16, n, nb, k, w)
+        ctx.build_fixed_dev_new(mem, 16, n, nb, k, w)
         ctx.probe_dev([(w, nb, k)], q, 2 * n, out, key_len=16)
     torch.cuda.synchronize(dev)
     ev[0].record()
     for _ in range(reps):
-        w.zero_()
-        ctx.build_fixed_dev(mem, 16, n, nb, k, w)
+        ctx.build_fixed_dev_new(mem, 16, n, nb, k, w)
     ev[1].record()
     ev[2].record()
     for _ in range(reps):
@@ -540,7 +549,7 @@ def bench_c1_gpu(ctx, dev, reps=20):
     torch.cuda.synchronize(dev)
     b_ms, p_ms = ev[0].elapsed_time(ev[1]) / reps, ev[2].elapsed_time(ev[3]) / reps
     res = {"workload": "C1 (configs[0]) on the GPU: build new(%d, 0.01) (%d bits, k=%d) from %d key16 members "
-                       "(zero + build), probe %d members + %d non-members" % (n, nb, k, n, n, n),
+                       "(lsmb_build_fixed_dev_new), probe %d members + %d non-members" % (n, nb, k, n, n, n),
            "build": {"ms": round(b_ms, 4), "value": round(n / (b_ms * 1e-3) / 1e6, 1), "unit": "Mkeys/s",
                      "strategy": lsmbloom.build_strategy(nb, n, k)},
            "probe": {"ms": round(p_ms, 4), "value": round(2 * n / (p_ms * 1e-3) / 1e6, 1), "unit": "Mkeys/s"}}
@@ -571,8 +580,7 @@ def bench_exact10(ctx, keys, n, reps=10):
     ctx.set_timing(True)
     kt = np.zeros(3)
     for i in range(reps + 2):
-        w.zero_()
-        ctx.build_fixed_dev(keys, 16, n, nb, k, w)
+        ctx.build_fixed_dev_new(keys, 16, n, nb, k, w)
         ctx.sync()
         torch.cuda.synchronize(keys.device)
         if i >= 2:
@@ -706,8 +714,7 @@ def bench_varlen(ctx, dev, args):
     words = torch.zeros(nw, dtype=torch.int64, device=dev)
 
     def step():
-        words.zero_()
-        ctx.build_var_dev(data, offs, n, nb, k, words)
+        ctx.build_var_dev_new(data, offs, n, nb, k, words)
 
     ctx.set_timing(False)
     for _ in range(max(1, args.warmup // 2)):
@@ -722,8 +729,7 @@ def bench_varlen(ctx, dev, args):
     ctx.set_timing(True)
     kt = np.zeros(3)
     for _ in range(steps):
-        words.zero_()
-        ctx.build_var_dev(data, offs, n, nb, k, words)
+        ctx.build_var_dev_new(data, offs, n, nb, k, words)
         ctx.sync()
         kt += np.array(ctx.last_build_ms())
     kt /= steps

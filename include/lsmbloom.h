@@ -201,6 +201,16 @@ int lsmb_build_fixed_dev(lsmb_ctx* ctx, const void* d_keys, uint32_t key_len, ui
 int lsmb_build_var_dev(lsmb_ctx* ctx, const void* d_data, const void* d_offsets, uint64_t n,
                        uint32_t num_bits, uint32_t num_hashes, void* d_words, void* stream);
 
+/* BloomFilterBuilder::{new, add_key per key, build} (src/bloom/builder.rs:14-28) into device words:
+ * BloomFilter::new (src/bloom/mod.rs:38-67) + insert of every key.  Unlike the
+ * entry points above, `d_words` is OUTPUT-ONLY — its old contents are ignored,
+ * every word of the filter is written — so the build needs no zeroing pass and
+ * never reads the old words.  n == 0 or num_hashes == 0 writes all-zero words. */
+int lsmb_build_fixed_dev_new(lsmb_ctx* ctx, const void* d_keys, uint32_t key_len, uint64_t n,
+                             uint32_t num_bits, uint32_t num_hashes, void* d_words, void* stream);
+int lsmb_build_var_dev_new(lsmb_ctx* ctx, const void* d_data, const void* d_offsets, uint64_t n,
+                           uint32_t num_bits, uint32_t num_hashes, void* d_words, void* stream);
+
 /* A partitioned build (filters above a few MiB) runs in sweeps: each re-reads
  * the keys and keeps the positions of its own range of the filter (C5's
  * 2^32-1-bit filter: 2 sweeps of 256 MiB).  lsmb_build_sweeps gives their
@@ -214,6 +224,11 @@ int lsmb_sweep_words(uint32_t num_bits, uint32_t num_hashes, uint64_t n, int swe
                      uint64_t* word_hi);
 int lsmb_build_fixed_dev_sweep(lsmb_ctx* ctx, const void* d_keys, uint32_t key_len, uint64_t n,
                                uint32_t num_bits, uint32_t num_hashes, void* d_words, int sweep, void* stream);
+/* Sweep s of lsmb_build_fixed_dev_new: writes every word of sweep s's range
+ * [word_lo, word_hi) (output-only there), no other word.  Running every sweep
+ * == lsmb_build_fixed_dev_new. */
+int lsmb_build_fixed_dev_sweep_new(lsmb_ctx* ctx, const void* d_keys, uint32_t key_len, uint64_t n,
+                                   uint32_t num_bits, uint32_t num_hashes, void* d_words, int sweep, void* stream);
 
 /* CRC-32 of bloom blocks (optional checksum; the reference's
  * bloom block has none).  The same CRC as crc32fast::hash / zlib.crc32, which

@@ -163,6 +163,16 @@ struct PassA {
     uint64_t* regions;      // [grid][nbins][cap][8] u64: workgroup w's regions are contiguous
     uint32_t* counts;       // [nbins][grid] segments written
     uint32_t* gw;           // filter words (ring / region overflow only)
+    // Fresh builds (k_bin<..., LIST = true>, see or_pos_list): a position
+    // past its ring or region goes to the workgroup's list ovl[w][0, ovl_cap)
+    // (length in ovn[w]), which k_ovf_apply ORs into the filter after pass B;
+    // past a full list, its bit goes to the all-zero overflow words `ovf` and
+    // its 2^20-bit unit is marked in `dirty`, which pass B folds in and clears.
+    uint32_t* ovf;
+    uint32_t* dirty;
+    uint32_t* ovl;
+    uint32_t* ovn;
+    uint32_t ovl_cap;
     uint32_t* err;          // device counters (LSMB_STATS builds)
 };
 
@@ -183,6 +193,20 @@ template <int SL = kSliceLog2>
 __device__ __forceinline__ void or_pos_global(uint32_t* gw, uint32_t b, uint32_t off) {
     const uint32_t p = (b << SL) | off;
     atomicOr(gw + (p >> 5), 1u << (p & 31));
+}
+
+// The overflow path of a fresh build: a fresh build's pass B writes every
+// filter word without reading it, so pass A must not touch the words.
+template <int SL = kSliceLog2>
+__device__ __forceinline__ void or_pos_list(const PassA& a, uint32_t* ovn_lds, uint32_t w, uint32_t b, uint32_t off) {
+    const uint32_t p = (b << SL) | off;
+    const uint32_t i = atomicAdd(ovn_lds, 1u);
+    if (i < a.ovl_cap) {
+        a.ovl[(uint64_t)w * a.ovl_cap + i] = p;
+    } else {
+        atomicOr(a.ovf + (p >> 5), 1u << (p & 31));
+        a.dirty[p >> kSliceLog2] = 1u;
+    }
 }
 
 // Three SL-bit offsets (SL = 20 or 21) in one u64: x | y << SL | z << 2 SL,
@@ -232,7 +256,9 @@ constexpr uint32_t kAhead = 4;  // pass A key prefetch distance, in phases
 // flush rounds per key (PartitionPlan::keys_per_lane; the ring is sized for it).
 // SL: bin width log2 (20; 21 for sweeps of filters above 2^30 bits, whose
 // pass B applies each bin as two 2^20-bit halves).
-template <class Src, class W, int KMAX, bool EXACT, bool FULL, int PER = 1, int SL = kSliceLog2>
+// LIST: a fresh build's pass A (overflow to the lists, or_pos_list); the
+// OR-accumulate kernels set overflow bits in the filter words directly.
+template <class Src, class W, int KMAX, bool EXACT, bool FULL, int PER = 1, int SL = kSliceLog2, bool LIST = false>
 __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md, uint32_t k_, PassA a) {
     static_assert(PER == 1 || EXACT, "two keys per lane: exact k only");
     constexpr uint32_t kMask = (1u << SL) - 1;
@@ -244,7 +270,17 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
     // per-wave flush job tables, 16-B aligned after the fill words
     uint4* jobtab = reinterpret_cast<uint4*>(sm + ((((size_t)(nb + 1) * (R + 1)) + 3) & ~(size_t)3));
     const uint32_t tid = threadIdx.x, w = blockIdx.x, lane = tid & 63, wave = tid >> 6;
+    // overflow list length (LIST): the word after the job tables
+    uint32_t* ovn = reinterpret_cast<uint32_t*>(jobtab + (kBinBlock / 64) * kBinJobsPerWave);
     for (uint32_t i = tid; i <= nb; i += kBinBlock) fill[i] = 0;
+    if (LIST && tid == 0) *ovn = 0;
+    // a position past its ring or region
+    auto overflow = [&](uint32_t b, uint32_t off) {
+        if constexpr (LIST)
+            or_pos_list<SL>(a, ovn, w, b, off);
+        else
+            or_pos_global<SL>(a.gw, b, off);
+    };
     // Workgroup w's regions as a raw buffer: a store at an offset past
     // num_records is dropped by the hardware, which lets every lane issue the
     // flush stores unconditionally (see the flush).
@@ -384,7 +420,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
                     if (got[q] < lim) {
                         *(uint32_t*)((char*)sm + slot(q)) = pos[q] & kMask;
                     } else if (pos[q] < sink) {  // (the sink's claims add 0: never past its ring)
-                        or_pos_global<SL>(a.gw, a.b0 + (pos[q] >> SL), pos[q] & kMask);
+                        overflow(a.b0 + (pos[q] >> SL), pos[q] & kMask);
 #ifdef LSMB_STATS
                         atomicAdd(a.err + 9, 1u);
 #endif
@@ -448,10 +484,20 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
             }
         };
         auto spill_segment = [&]() {  // region full (adversarial inputs): exact global atomics
-            const uint32_t vals[24] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w,
-                                       y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w,
-                                       z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
-            for (int t = 0; t < 24; t++) or_pos_global<SL>(a.gw, a.b0 + own, vals[t]);
+            if constexpr (LIST) {
+                // (rolled over the ring: one inlined list append per site, not 24)
+#pragma unroll 1
+                for (uint32_t t = 0; t < (uint32_t)kSegEntries; t++) {
+                    uint32_t e = start + 4 * t;
+                    e = min(e, e - R4);
+                    overflow(a.b0 + own, *(const uint32_t*)(ring + e));
+                }
+            } else {
+                const uint32_t vals[24] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w,
+                                           y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w,
+                                           z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
+                for (int t = 0; t < 24; t++) or_pos_global<SL>(a.gw, a.b0 + own, vals[t]);
+            }
 #ifdef LSMB_STATS
             atomicAdd(a.err + 7, 24u);
 #endif
@@ -567,13 +613,30 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
                 for (int t = 0; t < kSegWords; t++) dst[t] = pack3<SL>(v[t], v[t + 8], v[t + 16]);
                 segs++;
             } else {
-                for (uint32_t t = 0; t < m; t++) or_pos_global<SL>(a.gw, a.b0 + own, v[t]);
+                for (uint32_t t = 0; t < m; t++) overflow(a.b0 + own, v[t]);
             }
             const uint32_t s = start + 4 * m;
             start = min(s, s - R4);
             cnt -= m;
         }
         a.counts[(uint64_t)(a.b0 + own) * a.grid + w] = segs;
+    }
+    if constexpr (LIST) {  // the overflow list's length, for k_ovf_apply
+        __syncthreads();
+        if (tid == 0) a.ovn[w] = min(*ovn, a.ovl_cap);
+    }
+}
+
+// Fresh partition builds, after pass B: OR the positions pass A listed as
+// overflow (PassA::ovl) into the filter with global atomics.  Block w takes
+// list w (pass A workgroup w of a sweep).
+__global__ __launch_bounds__(256) void k_ovf_apply(const uint32_t* __restrict__ ovl, const uint32_t* __restrict__ ovn,
+                                                   uint32_t cap, uint32_t* __restrict__ gw) {
+    const uint32_t w = blockIdx.x, n = ovn[w];
+    const uint32_t* l = ovl + (uint64_t)w * cap;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint32_t p = l[i];
+        atomicOr(gw + (p >> 5), 1u << (p & 31));
     }
 }
 
@@ -586,6 +649,9 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
 //      region's 16-B pieces are loaded U per lane at a time and every 20-bit
 //      offset is ORed into LDS;
 //   3. the slice is written back once.
+// fresh (BloomFilter::new + inserts, LIST pass A): the slice starts from zero
+// instead of its words in HBM, which are then write-only; a unit marked in
+// `dirty` ORs in (and clears) its overflow words.
 // SL = 21 (2^21-bit bins): a bin is applied as two 2^20-bit halves by two
 // workgroups, each reading all of the bin's offsets and keeping its own.
 // Units u -> (bin, half) so that the two halves of a bin are blocks u and
@@ -597,7 +663,9 @@ __global__ __launch_bounds__(kApplyBlock) void k_apply(const uint64_t* __restric
                                                        const uint32_t* __restrict__ counts,
                                                        uint32_t grid, uint32_t cap, uint32_t nbins,
                                                        uint32_t* __restrict__ gw, uint64_t nw32,
-                                                       uint32_t bfirst, uint32_t bend) {
+                                                       uint32_t bfirst, uint32_t bend,
+                                                       uint32_t* __restrict__ ovf, uint32_t* __restrict__ dirty,
+                                                       uint32_t fresh) {
     constexpr uint32_t H = 1u << (SL - kSliceLog2);  // 2^20-bit halves per bin
     constexpr uint32_t kMask = (1u << SL) - 1;
     __shared__ uint32_t filt[kSliceWords32];
@@ -618,17 +686,29 @@ __global__ __launch_bounds__(kApplyBlock) void k_apply(const uint64_t* __restric
         const uint32_t nw2 = (uint32_t)min((uint64_t)kSliceWords32, nw32 - w0) / 2;  // u64 words
         uint2* g2 = reinterpret_cast<uint2*>(gw + w0);
         uint2* f2 = reinterpret_cast<uint2*>(filt);
+        const uint32_t unit = (uint32_t)(w0 / kSliceWords32);
+        const bool dty = dirty && dirty[unit] != 0u;  // block-uniform (fresh builds only)
         {
             uint2 v[PER];
 #pragma unroll
             for (uint32_t u = 0; u < PER; u++) {
                 const uint32_t i = tid + u * kApplyBlock;
-                v[u] = i < nw2 ? g2[i] : make_uint2(0, 0);
+                v[u] = (i < nw2 && !fresh) ? g2[i] : make_uint2(0, 0);
             }
 #pragma unroll
             for (uint32_t u = 0; u < PER; u++) {
                 const uint32_t i = tid + u * kApplyBlock;
                 if (i < nw2) f2[i] = v[u];
+            }
+        }
+        if (__builtin_expect(dty, 0)) {  // (rolled, after the slice load: no registers held across)
+            uint2* o2 = reinterpret_cast<uint2*>(ovf + w0);
+#pragma unroll 1
+            for (uint32_t i = tid; i < nw2; i += kApplyBlock) {
+                const uint2 o = o2[i];
+                f2[i].x |= o.x;
+                f2[i].y |= o.y;
+                o2[i] = make_uint2(0, 0);
             }
         }
         const uint32_t nreg = wave < grid ? (grid - 1 - wave) / NWAVE + 1 : 0;  // <= 64 (grid <= 1024)
@@ -667,6 +747,7 @@ __global__ __launch_bounds__(kApplyBlock) void k_apply(const uint64_t* __restric
         }
         __syncthreads();
         for (uint32_t i = tid; i < nw2; i += kApplyBlock) g2[i] = f2[i];
+        if (dty && tid == 0) dirty[unit] = 0u;  // every thread read it before the first barrier
         __syncthreads();
     }
 }
@@ -751,7 +832,7 @@ void launch_hash_var(const VarLen& src, uint64_t n, Out out, hipStream_t st) {
 template <class Src>
 hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k, uint32_t* gw,
                       BuildStrategy s, const PartitionWorkspace& ws, int num_cus, hipStream_t st,
-                      BuildTimers* tm, int sweep, bool t0_done = false) {
+                      BuildTimers* tm, int sweep, bool fresh, bool t0_done = false) {
     const Mod32 md = Mod32::make(num_bits);
     // sweep >= 0 (partition builds): only that sweep's slices — pass A keeps
     // their positions, pass B applies them; every other strategy has one sweep
@@ -759,6 +840,12 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
     const uint32_t nw32 = (uint32_t)(2 * (((uint64_t)num_bits + 63) / 64));
     if (tm && !t0_done) hipEventRecord(tm->t0, st);
     constexpr bool kRecSrc = std::is_same<Src, ks::Recs>::value;  // walk records: partition builds only
+    // fresh: the words are output-only.  Single-sweep k = 7 partition builds
+    // write every word in pass B without reading it; the rest start from zeros.
+    if (fresh && s != BuildStrategy::Partition) {
+        const hipError_t e = hipMemsetAsync(gw, 0, (size_t)nw32 * 4, st);
+        if (e != hipSuccess) return e;
+    }
     if (s != BuildStrategy::Partition) {
       if constexpr (kRecSrc) {
         return hipErrorInvalidValue;
@@ -816,10 +903,28 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
             k_hash<Src, OutRec><<<dim3((uint32_t)g), dim3(256), 0, st>>>(src, n, rec);
         // pass A's timer (t1) covers k_hash + k_bin
         return build_with(ks::Recs{reinterpret_cast<const uint32_t*>(ws.hashes)}, n, num_bits, k, gw, s, ws, num_cus,
-                          st, tm, sweep, /*t0_done=*/true);
+                          st, tm, sweep, fresh, /*t0_done=*/true);
     } else {
         const PartitionPlan pl = plan_partition(num_bits, k, n, num_cus);
         if (pl.region_bytes > ws.region_bytes || pl.counts_bytes > ws.counts_bytes) return hipErrorInvalidValue;
+        const uint32_t bfirst = sweep >= 0 ? (uint32_t)sweep * pl.bins_per_sweep : 0u;
+        const uint32_t bend = sweep >= 0 ? min(pl.nbins, bfirst + pl.bins_per_sweep) : pl.nbins;
+        // Fresh builds: single-sweep k = 7 plans run the LIST pass A and a pass
+        // B that never reads the words; others (multi-sweep plans keep their
+        // two-key phases, whose ~0.45 % ring overflow a list would pay for)
+        // zero their word range first and accumulate.
+        const bool list = fresh && k == 7 && pl.sweeps == 1;
+        if (list && (!ws.ovf || !ws.dirty || ws.ovf_units * kSliceWords32 < nw32 || !ws.ovl ||
+                     ws.ovl_groups < pl.grid))
+            return hipErrorInvalidValue;
+        if (fresh && !list) {
+            const uint64_t wlo = (uint64_t)bfirst << (pl.slice_log2 - 5);
+            const uint64_t whi = min((uint64_t)nw32, (uint64_t)bend << (pl.slice_log2 - 5));
+            if (whi > wlo) {
+                const hipError_t e = hipMemsetAsync(gw + wlo, 0, (size_t)(whi - wlo) * 4, st);
+                if (e != hipSuccess) return e;
+            }
+        }
         const bool w32 = fits_walk32(num_bits);
         // walks: from (h1, h2), or replayed from 12-B records
         constexpr bool kRec = std::is_same<Src, ks::Recs>::value;
@@ -836,6 +941,11 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
             a.regions = ws.regions;
             a.counts = ws.counts;
             a.gw = gw;
+            a.ovf = ws.ovf;
+            a.dirty = ws.dirty;
+            a.ovl = ws.ovl;
+            a.ovn = ws.ovn;
+            a.ovl_cap = kOvfListCap;
             a.err = ws.err;
             a.nbins = pl.nbins;
             const size_t smem = (size_t)(a.nb + 1) * (4 * a.ring + kBinExtraBytes) + kBinJobBytes;
@@ -847,7 +957,10 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
             auto go7 = [&](auto slc) {  // k = 7 (BloomFilter::new at fpr 0.01), bin width 2^SL
                 constexpr int SL = decltype(slc)::value;
                 const bool two = pl.keys_per_lane == 2;
-                if (w32) {
+                if (list && !two) {  // (full: list builds are single-sweep)
+                    if (w32) go(k_bin<Src, Walk32, 7, true, true, 1, SL, true>);
+                    else go(k_bin<Src, Walk64, 7, true, true, 1, SL, true>);
+                } else if (w32) {
                     if (full && two) go(k_bin<Src, Walk32, 7, true, true, 2, SL>);
                     else if (full) go(k_bin<Src, Walk32, 7, true, true, 1, SL>);
                     else if (two) go(k_bin<Src, Walk32, 7, true, false, 2, SL>);
@@ -888,16 +1001,16 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
         }
 #endif
         if (tm) hipEventRecord(tm->t1, st);
-        const uint32_t bfirst = sweep >= 0 ? (uint32_t)sweep * pl.bins_per_sweep : 0u;
-        const uint32_t bend = sweep >= 0 ? min(pl.nbins, bfirst + pl.bins_per_sweep) : pl.nbins;
         if (bend > bfirst) {
+            uint32_t* dmark = list ? ws.dirty : nullptr;
             if (pl.slice_log2 == 21)
                 k_apply<21><<<dim3(2 * (bend - bfirst)), dim3(kApplyBlock), 0, st>>>(
-                    ws.regions, ws.counts, pl.grid, pl.cap_segs, pl.nbins, gw, nw32, bfirst, bend);
+                    ws.regions, ws.counts, pl.grid, pl.cap_segs, pl.nbins, gw, nw32, bfirst, bend, ws.ovf, dmark, list);
             else
                 k_apply<<<dim3(bend - bfirst), dim3(kApplyBlock), 0, st>>>(ws.regions, ws.counts, pl.grid,
                                                                            pl.cap_segs, pl.nbins, gw, nw32, bfirst,
-                                                                           bend);
+                                                                           bend, ws.ovf, dmark, list);
+            if (list) k_ovf_apply<<<dim3(pl.grid), dim3(256), 0, st>>>(ws.ovl, ws.ovn, kOvfListCap, gw);
         }
     }
     if (tm) {
@@ -1047,13 +1160,17 @@ uint64_t partition_chunk_keys(uint32_t num_bits, uint32_t k, uint64_t max_bytes,
 
 hipError_t launch_build(const KeyBatch& kb, uint32_t num_bits, uint32_t k, uint32_t* gw,
                         BuildStrategy s, const PartitionWorkspace& ws, int num_cus, hipStream_t st,
-                        BuildTimers* tm, int sweep) {
-    if (s == BuildStrategy::None) return hipSuccess;
-    if (kb.offsets) return build_with(VarLen{kb.data, kb.offsets}, kb.n, num_bits, k, gw, s, ws, num_cus, st, tm, sweep);
+                        BuildTimers* tm, int sweep, bool fresh) {
+    if (s == BuildStrategy::None) {
+        if (!fresh || num_bits == 0) return hipSuccess;
+        return hipMemsetAsync(gw, 0, (size_t)(((uint64_t)num_bits + 63) / 64) * 8, st);  // new(), no inserts
+    }
+    if (kb.offsets)
+        return build_with(VarLen{kb.data, kb.offsets}, kb.n, num_bits, k, gw, s, ws, num_cus, st, tm, sweep, fresh);
     if (kb.key_len == 16 && (reinterpret_cast<uintptr_t>(kb.data) & 15) == 0)
         return build_with(Fixed16{reinterpret_cast<const uint4*>(kb.data)}, kb.n, num_bits, k, gw, s, ws,
-                          num_cus, st, tm, sweep);
-    return build_with(FixedN{kb.data, kb.key_len}, kb.n, num_bits, k, gw, s, ws, num_cus, st, tm, sweep);
+                          num_cus, st, tm, sweep, fresh);
+    return build_with(FixedN{kb.data, kb.key_len}, kb.n, num_bits, k, gw, s, ws, num_cus, st, tm, sweep, fresh);
 }
 
 hipError_t launch_or_reduce(uint32_t* dst, const uint32_t* src, uint64_t nw32, uint32_t nsrc,

@@ -96,28 +96,31 @@ void report_stats(lsmb_ctx* c) {
 
 namespace {
 int build_dev_ws(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k, uint32_t* dw, hipStream_t st,
-                 BuildStrategy s, int sweep);
+                 BuildStrategy s, int sweep, bool fresh);
 }  // namespace
 
 // Device build of one batch, chunked so the partition workspace stays bounded.
 int build_dev(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k, uint32_t* dw,
-              hipStream_t st, int sweep) {
+              hipStream_t st, int sweep, bool fresh) {
     BuildStrategy s = pick_build_strategy(num_bits, k, kb_all.n);
     // LSMB_FORCE_STRATEGY=atomic: measurement override;
     // the filter is the same either way.
     if (const char* f = getenv("LSMB_FORCE_STRATEGY"))
         if ((s == BuildStrategy::Partition || s == BuildStrategy::Tiled) && !strcmp(f, "atomic")) s = BuildStrategy::Atomic;
     c->tm.valid = false;
-    if (s == BuildStrategy::None) return LSMB_OK;
+    if (s == BuildStrategy::None) {  // fresh: new() with no inserts, all-zero words
+        if (fresh && num_bits) HIP_TRY(hipMemsetAsync(dw, 0, nwords64(num_bits) * 8, st));
+        return LSMB_OK;
+    }
     if (s != BuildStrategy::Tiled && s != BuildStrategy::Partition)
-        return build_dev_ws(c, kb_all, num_bits, k, dw, st, s, sweep);
+        return build_dev_ws(c, kb_all, num_bits, k, dw, st, s, sweep, fresh);
     // Tiled and partition builds use the context's shared workspace: a build
     // issued on a different stream than the last one waits for it (two
     // streams' builds would otherwise overwrite each other's regions).  On the
     // same stream, stream order already serialises them: no wait packet (a
     // barrier packet between consecutive builds costs the stream ~10 us).
     if (c->ws_stream && c->ws_stream != st) HIP_TRY(hipStreamWaitEvent(st, c->ws_done, 0));
-    const int rc = build_dev_ws(c, kb_all, num_bits, k, dw, st, s, sweep);
+    const int rc = build_dev_ws(c, kb_all, num_bits, k, dw, st, s, sweep, fresh);
     HIP_TRY(hipEventRecord(c->ws_done, st));
     c->ws_stream = st;
     return rc;
@@ -125,7 +128,7 @@ int build_dev(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k
 
 namespace {
 int build_dev_ws(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k, uint32_t* dw, hipStream_t st,
-                 BuildStrategy s, int sweep) {
+                 BuildStrategy s, int sweep, bool fresh) {
     if (s == BuildStrategy::Tiled) {
         const TiledPlan tp = plan_tiled(num_bits, kb_all.n, c->num_cus);
         HIP_TRY(c->ws_regions.ensure(tp.scratch_bytes));
@@ -137,12 +140,13 @@ int build_dev_ws(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_
             ws.hashes = (uint4*)c->ws_hashes.p;
             ws.hash_bytes = c->ws_hashes.bytes;
         }
-        HIP_TRY(launch_build(kb_all, num_bits, k, dw, s, ws, c->num_cus, st, c->timing ? &c->tm : nullptr, sweep));
+        HIP_TRY(launch_build(kb_all, num_bits, k, dw, s, ws, c->num_cus, st, c->timing ? &c->tm : nullptr, sweep,
+                             fresh));
         return LSMB_OK;
     }
     if (s != BuildStrategy::Partition) {
         HIP_TRY(launch_build(kb_all, num_bits, k, dw, s, PartitionWorkspace{}, c->num_cus, st,
-                             c->timing ? &c->tm : nullptr, sweep));
+                             c->timing ? &c->tm : nullptr, sweep, fresh));
         return LSMB_OK;
     }
     uint64_t chunk = partition_chunk_keys(num_bits, k, workspace_limit_bytes(), c->num_cus);
@@ -157,6 +161,25 @@ int build_dev_ws(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_
     ws.err = (uint32_t*)c->err.p;
     ws.region_bytes = c->ws_regions.bytes;
     ws.counts_bytes = c->ws_counts.bytes;
+    if (fresh && k == 7 && pl.sweeps == 1) {
+        // a fresh single-sweep build (the LIST pass A, bloom_build.hip): the
+        // overflow lists, and the overflow words + unit marks of the whole
+        // filter for lists that fill up, zeroed once when (re)allocated
+        const uint64_t units = ((nwords64(num_bits) * 2) + kSliceWords32 - 1) / kSliceWords32;
+        const size_t ob = c->ws_ovf.bytes, db = c->ws_dirty.bytes;
+        HIP_TRY(c->ws_ovf.ensure(units * kSliceWords32 * 4));
+        HIP_TRY(c->ws_dirty.ensure(units * 4));
+        if (c->ws_ovf.bytes != ob) HIP_TRY(hipMemsetAsync(c->ws_ovf.p, 0, c->ws_ovf.bytes, st));
+        if (c->ws_dirty.bytes != db) HIP_TRY(hipMemsetAsync(c->ws_dirty.p, 0, c->ws_dirty.bytes, st));
+        ws.ovf = (uint32_t*)c->ws_ovf.p;
+        ws.dirty = (uint32_t*)c->ws_dirty.p;
+        ws.ovf_units = std::min<uint64_t>(c->ws_ovf.bytes / (kSliceWords32 * 4), c->ws_dirty.bytes / 4);
+        HIP_TRY(c->ws_ovl.ensure((uint64_t)pl.grid * kOvfListCap * 4));
+        HIP_TRY(c->ws_ovn.ensure((uint64_t)pl.grid * 4));
+        ws.ovl = (uint32_t*)c->ws_ovl.p;
+        ws.ovn = (uint32_t*)c->ws_ovn.p;
+        ws.ovl_groups = (uint32_t)std::min<uint64_t>(c->ws_ovn.bytes / 4, c->ws_ovl.bytes / (kOvfListCap * 4ull));
+    }
     const bool fixed16 = !kb_all.offsets && kb_all.key_len == 16 && (reinterpret_cast<uintptr_t>(kb_all.data) & 15) == 0;
     if (!fixed16) {  // pre-hashed pass A (ks::Hashed): 16 B per key of the chunk
         HIP_TRY(c->ws_hashes.ensure(chunk * 16));
@@ -170,7 +193,9 @@ int build_dev_ws(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_
             kb.offsets += first;  // VarLen offsets are absolute into data
         else
             kb.data += first * kb.key_len;
-        HIP_TRY(launch_build(kb, num_bits, k, dw, s, ws, c->num_cus, st, c->timing ? &c->tm : nullptr, sweep));
+        // fresh: the first chunk writes every word of the range, the rest accumulate
+        HIP_TRY(launch_build(kb, num_bits, k, dw, s, ws, c->num_cus, st, c->timing ? &c->tm : nullptr, sweep,
+                             fresh && first == 0));
     }
     return LSMB_OK;
 }
@@ -540,7 +565,7 @@ void lsmb_close(lsmb_ctx* c) {
         DevGuard g(c->dev);
         hipStreamSynchronize(c->st);
         if (c->cst) hipStreamSynchronize(c->cst);
-        for (DevBuf* b : {&c->ws_regions, &c->ws_counts, &c->ws_hashes, &c->crc_parts, &c->err, &c->keys, &c->offs, &c->words, &c->out,
+        for (DevBuf* b : {&c->ws_regions, &c->ws_counts, &c->ws_hashes, &c->ws_ovf, &c->ws_dirty, &c->ws_ovl, &c->ws_ovn, &c->crc_parts, &c->err, &c->keys, &c->offs, &c->words, &c->out,
                           &c->filt_words, &c->filt_desc, &c->kslot[0], &c->kslot[1], &c->oslot[0], &c->oslot[1]})
             b->release();
         for (int s = 0; s < 2; s++) {
@@ -596,6 +621,30 @@ int lsmb_build_var_dev(lsmb_ctx* c, const void* d_data, const void* d_offsets, u
     return build_dev(c, kb, num_bits, k, (uint32_t*)d_words, pick_stream(c, stream));
 }
 
+// BloomFilterBuilder::{new, add_key, build} (src/bloom/builder.rs:14-28): BloomFilter::new
+// (src/bloom/mod.rs:38-67, all-zero words) + insert of every key.  The words
+// are output-only: the partition build writes each of them once in pass B
+// without reading it, so no zeroing pass and no read of the old words.
+int lsmb_build_fixed_dev_new(lsmb_ctx* c, const void* d_keys, uint32_t key_len, uint64_t n, uint32_t num_bits,
+                             uint32_t k, void* d_words, void* stream) {
+    if (!c) return fail(LSMB_EINVAL, "null ctx");
+    if (int rc = check_filter(num_bits, k)) return rc;
+    if (!d_words || (n && !d_keys)) return fail(LSMB_EINVAL, "null device pointer");
+    DevGuard g(c->dev);
+    KeyBatch kb{(const uint8_t*)d_keys, nullptr, key_len, key_len ? n : (n ? 1 : 0)};
+    return build_dev(c, kb, num_bits, k, (uint32_t*)d_words, pick_stream(c, stream), -1, /*fresh=*/true);
+}
+
+int lsmb_build_var_dev_new(lsmb_ctx* c, const void* d_data, const void* d_offsets, uint64_t n, uint32_t num_bits,
+                           uint32_t k, void* d_words, void* stream) {
+    if (!c) return fail(LSMB_EINVAL, "null ctx");
+    if (int rc = check_filter(num_bits, k)) return rc;
+    if (!d_words || (n && !d_offsets)) return fail(LSMB_EINVAL, "null device pointer");
+    DevGuard g(c->dev);
+    KeyBatch kb{(const uint8_t*)d_data, (const uint64_t*)d_offsets, 0, n};
+    return build_dev(c, kb, num_bits, k, (uint32_t*)d_words, pick_stream(c, stream), -1, /*fresh=*/true);
+}
+
 // Builds of n <= host_max_keys() keys run the library's host loop (no device
 // round trip, ctx may be NULL); bigger ones need a device context.
 static int need_ctx(lsmb_ctx* c, uint64_t n) {
@@ -638,6 +687,18 @@ int lsmb_build_fixed_dev_sweep(lsmb_ctx* c, const void* d_keys, uint32_t key_len
     DevGuard g(c->dev);
     KeyBatch kb{(const uint8_t*)d_keys, nullptr, key_len, key_len ? n : (n ? 1 : 0)};
     return build_dev(c, kb, num_bits, k, (uint32_t*)d_words, pick_stream(c, stream), sweep);
+}
+
+int lsmb_build_fixed_dev_sweep_new(lsmb_ctx* c, const void* d_keys, uint32_t key_len, uint64_t n, uint32_t num_bits,
+                                   uint32_t k, void* d_words, int sweep, void* stream) {
+    if (!c) return fail(LSMB_EINVAL, "null ctx");
+    if (int rc = check_filter(num_bits, k)) return rc;
+    if (!d_words || (n && !d_keys)) return fail(LSMB_EINVAL, "null device pointer");
+    const int ns = lsmb_build_sweeps(num_bits, k, n);
+    if (sweep < 0 || sweep >= ns) return fail(LSMB_EINVAL, "sweep %d out of range [0, %d)", sweep, ns);
+    DevGuard g(c->dev);
+    KeyBatch kb{(const uint8_t*)d_keys, nullptr, key_len, key_len ? n : (n ? 1 : 0)};
+    return build_dev(c, kb, num_bits, k, (uint32_t*)d_words, pick_stream(c, stream), sweep, /*fresh=*/true);
 }
 
 int lsmb_build_fixed(lsmb_ctx* c, const uint8_t* keys, uint32_t key_len, uint64_t n, uint32_t num_bits,

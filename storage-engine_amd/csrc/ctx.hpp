@@ -122,6 +122,8 @@ struct lsmb_ctx {
     lsmb::DevBuf crc_parts;              // CRC-32 workgroup partials (crc32.hip)
     lsmb::DevBuf ws_hashes;              // k_hash records (var-len / odd-length keys)
     lsmb::DevBuf err;                    // LSMB_STATS builds: pass A's overflow counters
+    lsmb::DevBuf ws_ovf, ws_dirty;       // partition: overflow words + unit marks (all-zero between builds)
+    lsmb::DevBuf ws_ovl, ws_ovn;         // fresh partition builds: overflow position lists + lengths
     // The workspace above is shared by every build on this context, whatever
     // stream it is issued on: ws_done marks the last build that used it, and a
     // build on another stream waits for it first (build_dev).
@@ -150,10 +152,11 @@ struct lsmb_ctx {
 
 namespace lsmb {
 
-// Device build of one batch on `st` into d_words (OR-accumulate), chunked so
-// the partition workspace stays bounded.  Asynchronous.
+// Device build of one batch on `st` into d_words (OR-accumulate; fresh =
+// BloomFilter::new + inserts: d_words is output-only), chunked so the
+// partition workspace stays bounded.  Asynchronous.
 int build_dev(lsmb_ctx* c, const KeyBatch& kb, uint32_t num_bits, uint32_t k, uint32_t* d_words, hipStream_t st,
-              int sweep = -1);
+              int sweep = -1, bool fresh = false);
 
 // Keys in host memory -> OR-accumulated into the device words dw (already
 // zeroed or loaded by the caller) on c->st: chunked H2D through the two

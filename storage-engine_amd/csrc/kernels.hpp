@@ -29,6 +29,7 @@ constexpr uint32_t kBinExtraBytes = 4;                // per slice besides its r
 constexpr uint32_t kMaxBinsPerSweep = 1024;           // one owner lane per slice: <= 64 slices per wave
 constexpr uint32_t kMaxRing = 1024;                   // ring entries per slice
 constexpr uint32_t kMaxRegionSegs = 1u << 24;         // region capacity bound (segments)
+constexpr uint32_t kOvfListCap = 16384;               // fresh builds: overflow positions listed per pass A workgroup
 
 // How a key batch is presented to the kernels.
 struct KeyBatch {
@@ -82,6 +83,17 @@ struct PartitionWorkspace {
     uint64_t* regions = nullptr;
     uint32_t* counts = nullptr;
     uint32_t* err = nullptr;  // device flag, see PassA::err
+    // Pass A's overflow bits (ring / region overflow, adversarial inputs) and
+    // per-2^20-bit-unit marks, both all-zero between builds (pass B clears
+    // what it consumes): ovf_units * 2^15 u32 words, ovf_units marks.
+    uint32_t* ovf = nullptr;
+    uint32_t* dirty = nullptr;
+    uint64_t ovf_units = 0;
+    // fresh builds: per pass A workgroup, a list of kOvfListCap overflow
+    // positions and its length (ovl_groups workgroups' worth)
+    uint32_t* ovl = nullptr;
+    uint32_t* ovn = nullptr;
+    uint32_t ovl_groups = 0;
     uint64_t region_bytes = 0;
     uint64_t counts_bytes = 0;
 };
@@ -91,14 +103,16 @@ struct BuildTimers {
     bool valid = false;
 };
 
-// Builds into d_words32 (OR-accumulate).  For the Partition strategy the
-// workspace must hold plan_partition(num_bits, k, kb.n, num_cus).  Records
+// Builds into d_words32 (OR-accumulate; fresh: BloomFilter::new + inserts,
+// the words are output-only and every word of the build's range is written).
+// For the Partition strategy the workspace must hold plan_partition(num_bits,
+// k, kb.n, num_cus) and the overflow words of the whole filter.  Records
 // t0/t1/t2 (start / pass A done / end) when timers != NULL.  sweep >= 0
 // builds only the bits of that partition sweep's slices (sweep 0 = the whole
 // build for the other strategies; see build_sweeps / sweep_words).
 hipError_t launch_build(const KeyBatch& kb, uint32_t num_bits, uint32_t k, uint32_t* d_words32,
                         BuildStrategy s, const PartitionWorkspace& ws, int num_cus,
-                        hipStream_t st, BuildTimers* timers, int sweep = -1);
+                        hipStream_t st, BuildTimers* timers, int sweep = -1, bool fresh = false);
 
 // Filter descriptor for the probe kernels (device-side array).
 struct ProbeFilter {

@@ -70,6 +70,10 @@ SIGNATURES = {
                                             ctypes.c_uint32, vp, vp]),
     "lsmb_build_var_dev": (ctypes.c_int, [vp, vp, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                           vp, vp]),
+    "lsmb_build_fixed_dev_new": (ctypes.c_int, [vp, vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
+                                                ctypes.c_uint32, vp, vp]),
+    "lsmb_build_var_dev_new": (ctypes.c_int, [vp, vp, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                              vp, vp]),
     "lsmb_probe_dev": (ctypes.c_int, [vp, ctypes.POINTER(vp), u32p, u32p, ctypes.c_uint32, vp, vp,
                                       ctypes.c_uint32, ctypes.c_uint64, vp, vp]),
     "lsmb_or_reduce_dev": (ctypes.c_int, [vp, vp, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, vp]),
@@ -91,6 +95,8 @@ SIGNATURES = {
     "lsmb_sweep_words": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, u64p, u64p]),
     "lsmb_build_fixed_dev_sweep": (ctypes.c_int, [vp, vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
                                                   ctypes.c_uint32, vp, ctypes.c_int, vp]),
+    "lsmb_build_fixed_dev_sweep_new": (ctypes.c_int, [vp, vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
+                                                      ctypes.c_uint32, vp, ctypes.c_int, vp]),
     "lsmb_set_host_max_keys": (None, [ctypes.c_uint64]),
     "lsmb_multi_open": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     "lsmb_multi_close": (None, [vp]),
@@ -144,6 +150,8 @@ def lib():
             raise ImportError("liblsmbloom.so not built (%s); run `make -C storage-engine_amd`" % LIB_PATH)
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("LSMB_LIB") and not hasattr(L, name):
+                continue  # an older library for an A/B run (tools/): entry points it predates stay unbound
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
@@ -326,6 +334,21 @@ class Context:
     def build_var_dev(self, data, offsets, n, num_bits, k, words, stream=None):
         _check(lib().lsmb_build_var_dev(self.h, vp(data.data_ptr()), vp(offsets.data_ptr()), n, num_bits, k,
                                         vp(words.data_ptr()), self._stream(stream)))
+
+    # BloomFilterBuilder::{new, add_key, build} (src/bloom/builder.rs:14-28):
+    # `words` is output-only, every word of the filter (of the sweep's range)
+    # is written; no zeroing pass, no read of the old words.
+    def build_fixed_dev_new(self, keys, key_len, n, num_bits, k, words, stream=None):
+        _check(lib().lsmb_build_fixed_dev_new(self.h, vp(keys.data_ptr() if n else 0), key_len, n, num_bits, k,
+                                              vp(words.data_ptr()), self._stream(stream)))
+
+    def build_fixed_dev_sweep_new(self, keys, key_len, n, num_bits, k, words, sweep, stream=None):
+        _check(lib().lsmb_build_fixed_dev_sweep_new(self.h, vp(keys.data_ptr() if n else 0), key_len, n, num_bits,
+                                                    k, vp(words.data_ptr()), int(sweep), self._stream(stream)))
+
+    def build_var_dev_new(self, data, offsets, n, num_bits, k, words, stream=None):
+        _check(lib().lsmb_build_var_dev_new(self.h, vp(data.data_ptr()), vp(offsets.data_ptr() if n else 0), n,
+                                            num_bits, k, vp(words.data_ptr()), self._stream(stream)))
 
     def probe_dev(self, filters, data, n, out, offsets=None, key_len=0, stream=None):
         """filters: [(words tensor on device, num_bits, k)]."""
