@@ -713,8 +713,15 @@ def bench_varlen(ctx, dev, args):
     nw = lsmbloom.num_words(nb)
     words = torch.zeros(nw, dtype=torch.int64, device=dev)
 
+    def build():
+        if args.accumulate:
+            words.zero_()
+            ctx.build_var_dev(data, offs, n, nb, k, words)
+        else:
+            ctx.build_var_dev_new(data, offs, n, nb, k, words)
+
     def step():
-        ctx.build_var_dev_new(data, offs, n, nb, k, words)
+        build()
 
     ctx.set_timing(False)
     for _ in range(max(1, args.warmup // 2)):
@@ -729,7 +736,7 @@ def bench_varlen(ctx, dev, args):
     ctx.set_timing(True)
     kt = np.zeros(3)
     for _ in range(steps):
-        ctx.build_var_dev_new(data, offs, n, nb, k, words)
+        build()
         ctx.sync()
         kt += np.array(ctx.last_build_ms())
     kt /= steps

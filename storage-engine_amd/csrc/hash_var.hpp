@@ -55,23 +55,42 @@ __device__ __forceinline__ uint32_t len_class(uint64_t len) {
 // Where a hash kernel puts key i's hash: the 16-B (h1, h2) record (filter
 // tiles, tools), or the 12-B walk record of a partitioned build (WalkRec:
 // h1 and h2 reduced mod num_bits plus the walk's carries).
+// kWords: the record's u32 words; words(): its contents; base(): record 0.
 struct OutH128 {
     uint4* p;
+    static constexpr uint32_t kWords = 4;
     __host__ __device__ OutH128(uint4* q) : p(q) {}
     __device__ __forceinline__ void put(uint64_t i, const H128& h) const {
         p[i] = make_uint4((uint32_t)h.lo, (uint32_t)(h.lo >> 32), (uint32_t)h.hi, (uint32_t)(h.hi >> 32));
     }
+    __device__ __forceinline__ void words(const H128& h, uint32_t* w) const {
+        w[0] = (uint32_t)h.lo, w[1] = (uint32_t)(h.lo >> 32), w[2] = (uint32_t)h.hi, w[3] = (uint32_t)(h.hi >> 32);
+    }
+    __device__ __forceinline__ uint32_t* base() const { return reinterpret_cast<uint32_t*>(p); }
 };
 struct OutRec {
     uint32_t* p;
     Mod32 md;
     uint32_t k;
+    static constexpr uint32_t kWords = 3;
     __device__ __forceinline__ void put(uint64_t i, const H128& h) const {
         const WalkRec q = WalkRec::make(md, h, k);
         uint32_t* o = p + 3 * i;
         o[0] = q.r, o[1] = q.s, o[2] = q.c;
     }
+    __device__ __forceinline__ void words(const H128& h, uint32_t* w) const {
+        const WalkRec q = WalkRec::make(md, h, k);
+        w[0] = q.r, w[1] = q.s, w[2] = q.c;
+    }
+    __device__ __forceinline__ uint32_t* base() const { return p; }
 };
+
+#ifndef LSMB_HV_REL
+#define LSMB_HV_REL 1  // key offsets handed to the sorted lanes through LDS (A/B knob)
+#endif
+#ifndef LSMB_HV_COAL
+#define LSMB_HV_COAL 1  // records staged in LDS and written as one coalesced block (A/B knob)
+#endif
 
 // WPE: waves per SIMD the register allocation must allow (0: compiler's
 // choice).  The hash paths want ~130 VGPRs; at <= 128 four waves fit a SIMD.
@@ -83,6 +102,9 @@ void k_hash_var(const uint8_t* __restrict__ d, const uint64_t* __restrict__ o, u
     __shared__ uint32_t win[WIN / 4 + 8];
     __shared__ uint32_t cls_cnt[16];
     __shared__ uint16_t perm[KEYS];
+    // the block's key offsets relative to its first (a block's keys span < 4 GiB)
+    __shared__ uint32_t rel[LSMB_HV_REL ? KEYS + 1 : 1];
+    static_assert(!LSMB_HV_COAL || KEYS * Out::kWords * 4 <= WIN, "records are staged in the window");
     const uint32_t t = threadIdx.x;
     const uint64_t i0 = (uint64_t)blockIdx.x * KEYS;
     const uint32_t m = (uint32_t)min<uint64_t>(KEYS, n - i0);
@@ -107,7 +129,15 @@ void k_hash_var(const uint8_t* __restrict__ d, const uint64_t* __restrict__ o, u
     }
     // lane assignment by length class (a counting sort of the block's keys)
     uint32_t cls = 15;
-    if (t < m) cls = MODE == 2 ? 0 : len_class(o[i0 + t + 1] - o[i0 + t]);  // MODE 2 (microbenchmark): no sort
+    const uint64_t kbase = o[i0];
+    if (t < m) {
+        const uint64_t a = o[i0 + t], b = o[i0 + t + 1];
+        cls = MODE == 2 ? 0 : len_class(b - a);  // MODE 2 (microbenchmark): no sort
+        if (LSMB_HV_REL) {
+            rel[t] = (uint32_t)(a - kbase);
+            if (t == m - 1) rel[m] = (uint32_t)(b - kbase);
+        }
+    }
     if (t < 16) cls_cnt[t] = 0;
     __syncthreads();
     const uint32_t rank = atomicAdd(&cls_cnt[cls], 1u);
@@ -119,8 +149,13 @@ void k_hash_var(const uint8_t* __restrict__ d, const uint64_t* __restrict__ o, u
     const uint32_t j = perm[t];  // the key this lane hashes
     uint64_t ka = 0, kb = 0;
     if (j < m) {
-        ka = o[i0 + j];
-        kb = o[i0 + j + 1];
+        if (LSMB_HV_REL) {  // (written before the perm barrier)
+            ka = kbase + rel[j];
+            kb = kbase + rel[j + 1];
+        } else {
+            ka = o[i0 + j];
+            kb = o[i0 + j + 1];
+        }
     }
     const uintptr_t end = (uintptr_t)(d + o[i0 + m]);  // one past the last key byte
     const uintptr_t pa = (uintptr_t)(d + ka), pb = (uintptr_t)(d + kb);
@@ -162,7 +197,30 @@ void k_hash_var(const uint8_t* __restrict__ d, const uint64_t* __restrict__ o, u
             f += c;
         }
     }
-    if (j < m) out.put(i0 + j, h);
+    if (!LSMB_HV_COAL) {
+        if (j < m) out.put(i0 + j, h);
+        return;
+    }
+    // The lanes hash keys in length-class order, so their records are
+    // scattered over the block's range: stage them in the window (every lane
+    // is past its last window read: the loop ends on a barrier) and write the
+    // block's records as one contiguous run of 16-B stores.
+    constexpr uint32_t W = Out::kWords;
+    if (j < m) {
+        uint32_t r[W];
+        out.words(h, r);
+#pragma unroll
+        for (uint32_t q = 0; q < W; q++) win[j * W + q] = r[q];
+    }
+    __syncthreads();
+    uint32_t* dst = out.base() + i0 * W;
+    const uint32_t nw = m * W;
+    if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+        for (uint32_t x = t; x < nw / 4; x += KEYS) reinterpret_cast<uint4*>(dst)[x] = reinterpret_cast<const uint4*>(win)[x];
+        for (uint32_t x = (nw & ~3u) + t; x < nw; x += KEYS) dst[x] = win[x];
+    } else {
+        for (uint32_t x = t; x < nw; x += KEYS) dst[x] = win[x];
+    }
 }
 
 }  // namespace lsmb

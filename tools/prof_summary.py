@@ -36,7 +36,7 @@ def traffic_json(d, out):
                 per[kn][cn] = sum(v) / len(v)
     kern = {}
     for kn, m in per.items():
-        if kn.startswith("k_bin<ks::Fixed16") or kn.startswith("k_apply"):
+        if kn.startswith(("k_bin<ks::Fixed16", "k_apply", "k_ovf_apply")):
             kern[kn] = {"read_bytes": int(2 * m.get("FETCH_SIZE", 0) * 1024),
                         "write_bytes": int(m.get("WRITE_SIZE", 0) * 1024),
                         "valu_insts": int(m.get("SQ_INSTS_VALU", 0))}
