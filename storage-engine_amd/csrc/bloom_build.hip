@@ -909,13 +909,14 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
         if (pl.region_bytes > ws.region_bytes || pl.counts_bytes > ws.counts_bytes) return hipErrorInvalidValue;
         const uint32_t bfirst = sweep >= 0 ? (uint32_t)sweep * pl.bins_per_sweep : 0u;
         const uint32_t bend = sweep >= 0 ? min(pl.nbins, bfirst + pl.bins_per_sweep) : pl.nbins;
-        // Fresh builds: single-sweep k = 7 plans run the LIST pass A and a pass
-        // B that never reads the words; others (multi-sweep plans keep their
-        // two-key phases, whose ~0.45 % ring overflow a list would pay for)
-        // zero their word range first and accumulate.
-        const bool list = fresh && k == 7 && pl.sweeps == 1;
+        // Fresh k = 7 builds run the LIST pass A (one key per lane per phase:
+        // the two-key phases of multi-sweep plans overflow ~0.45 % of C5's
+        // positions, which the lists would then OR in serially) and a pass B
+        // that never reads the words; other k zero their word range first and
+        // accumulate.
+        const bool list = fresh && k == 7;
         if (list && (!ws.ovf || !ws.dirty || ws.ovf_units * kSliceWords32 < nw32 || !ws.ovl ||
-                     ws.ovl_groups < pl.grid))
+                     ws.ovl_groups < pl.grid * pl.sweeps))
             return hipErrorInvalidValue;
         if (fresh && !list) {
             const uint64_t wlo = (uint64_t)bfirst << (pl.slice_log2 - 5);
@@ -943,8 +944,8 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
             a.gw = gw;
             a.ovf = ws.ovf;
             a.dirty = ws.dirty;
-            a.ovl = ws.ovl;
-            a.ovn = ws.ovn;
+            a.ovl = ws.ovl + (uint64_t)sw * pl.grid * kOvfListCap;  // one list per workgroup per sweep
+            a.ovn = ws.ovn + (uint64_t)sw * pl.grid;
             a.ovl_cap = kOvfListCap;
             a.err = ws.err;
             a.nbins = pl.nbins;
@@ -957,9 +958,11 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
             auto go7 = [&](auto slc) {  // k = 7 (BloomFilter::new at fpr 0.01), bin width 2^SL
                 constexpr int SL = decltype(slc)::value;
                 const bool two = pl.keys_per_lane == 2;
-                if (list && !two) {  // (full: list builds are single-sweep)
-                    if (w32) go(k_bin<Src, Walk32, 7, true, true, 1, SL, true>);
-                    else go(k_bin<Src, Walk64, 7, true, true, 1, SL, true>);
+                if (list) {
+                    if (w32 && full) go(k_bin<Src, Walk32, 7, true, true, 1, SL, true>);
+                    else if (w32) go(k_bin<Src, Walk32, 7, true, false, 1, SL, true>);
+                    else if (full) go(k_bin<Src, Walk64, 7, true, true, 1, SL, true>);
+                    else go(k_bin<Src, Walk64, 7, true, false, 1, SL, true>);
                 } else if (w32) {
                     if (full && two) go(k_bin<Src, Walk32, 7, true, true, 2, SL>);
                     else if (full) go(k_bin<Src, Walk32, 7, true, true, 1, SL>);
@@ -1010,7 +1013,11 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
                 k_apply<<<dim3(bend - bfirst), dim3(kApplyBlock), 0, st>>>(ws.regions, ws.counts, pl.grid,
                                                                            pl.cap_segs, pl.nbins, gw, nw32, bfirst,
                                                                            bend, ws.ovf, dmark, list);
-            if (list) k_ovf_apply<<<dim3(pl.grid), dim3(256), 0, st>>>(ws.ovl, ws.ovn, kOvfListCap, gw);
+            if (list) {  // the lists of the sweeps this call ran
+                const uint32_t s0 = sweep >= 0 ? (uint32_t)sweep : 0u, ns = sweep >= 0 ? 1u : pl.sweeps;
+                k_ovf_apply<<<dim3(ns * pl.grid), dim3(256), 0, st>>>(ws.ovl + (uint64_t)s0 * pl.grid * kOvfListCap,
+                                                                      ws.ovn + (uint64_t)s0 * pl.grid, kOvfListCap, gw);
+            }
         }
     }
     if (tm) {

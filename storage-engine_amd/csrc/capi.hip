@@ -161,10 +161,11 @@ int build_dev_ws(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_
     ws.err = (uint32_t*)c->err.p;
     ws.region_bytes = c->ws_regions.bytes;
     ws.counts_bytes = c->ws_counts.bytes;
-    if (fresh && k == 7 && pl.sweeps == 1) {
-        // a fresh single-sweep build (the LIST pass A, bloom_build.hip): the
-        // overflow lists, and the overflow words + unit marks of the whole
-        // filter for lists that fill up, zeroed once when (re)allocated
+    if (fresh && k == 7) {
+        // a fresh k = 7 build (the LIST pass A, bloom_build.hip): the overflow
+        // lists (per workgroup per sweep), and the overflow words + unit marks
+        // of the whole filter for lists that fill up, zeroed once when
+        // (re)allocated
         const uint64_t units = ((nwords64(num_bits) * 2) + kSliceWords32 - 1) / kSliceWords32;
         const size_t ob = c->ws_ovf.bytes, db = c->ws_dirty.bytes;
         HIP_TRY(c->ws_ovf.ensure(units * kSliceWords32 * 4));
@@ -174,8 +175,8 @@ int build_dev_ws(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_
         ws.ovf = (uint32_t*)c->ws_ovf.p;
         ws.dirty = (uint32_t*)c->ws_dirty.p;
         ws.ovf_units = std::min<uint64_t>(c->ws_ovf.bytes / (kSliceWords32 * 4), c->ws_dirty.bytes / 4);
-        HIP_TRY(c->ws_ovl.ensure((uint64_t)pl.grid * kOvfListCap * 4));
-        HIP_TRY(c->ws_ovn.ensure((uint64_t)pl.grid * 4));
+        HIP_TRY(c->ws_ovl.ensure((uint64_t)pl.grid * pl.sweeps * kOvfListCap * 4));
+        HIP_TRY(c->ws_ovn.ensure((uint64_t)pl.grid * pl.sweeps * 4));
         ws.ovl = (uint32_t*)c->ws_ovl.p;
         ws.ovn = (uint32_t*)c->ws_ovn.p;
         ws.ovl_groups = (uint32_t)std::min<uint64_t>(c->ws_ovn.bytes / 4, c->ws_ovl.bytes / (kOvfListCap * 4ull));
