@@ -1,4 +1,6 @@
 #!/bin/bash
+# (The variant libraries were built from the session tree with tools/build_variants.sh and LSMB_R3_VM /
+# LSMB_R3_FLUSH switches that were removed with the experiment; results in profiles/r03/r03_experiments.md.)
 # Ablation of the round-3 pass A changes, one box, accumulate builds (zero + lsmb_build_fixed_dev):
 # head (6c57a9a) | cur | novm (LSMB_R3_VM=0) | noflush (LSMB_R3_FLUSH=0) | neither; C2 and the C5 shard.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
