@@ -177,7 +177,7 @@ struct PassA {
 };
 
 __device__ __forceinline__ uint64_t* region_ptr(const PassA& a, uint32_t b, uint32_t w) {
-    return a.regions + ((uint64_t)w * a.nbins + b) * a.cap * kSegWords;
+    return a.regions + ((uint64_t)w * a.nbins + b) * a.cap * kSegSlotWords;
 }
 
 // Workgroup barrier that waits for this wave's LDS operations only.
@@ -285,7 +285,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
     // num_records is dropped by the hardware, which lets every lane issue the
     // flush stores unconditionally (see the flush).
     const __amdgpu_buffer_rsrc_t rgn = __builtin_amdgcn_make_buffer_rsrc(
-        region_ptr(a, 0, w), 0, (int)(a.nbins * a.cap * 64u), 0x00020000);
+        region_ptr(a, 0, w), 0, (int)(a.nbins * a.cap * kSegSlotBytes), 0x00020000);
     constexpr uint32_t kDrop = 0x80000000u;  // >= num_records (plan keeps it < 2^31)
     constexpr uint32_t kInc = 4u | (1u << 16);
     const uint32_t sink = nb << SL;  // local position of the sink slice
@@ -515,7 +515,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
                 g1 = min(g1, g1 - R4);
                 g2 = min(g2, g2 - R4);
                 jobtab[wave * kBinJobsPerWave + j] =
-                    make_uint4(rb + start, rb + g1, rb + g2, ((a.b0 + own) * a.cap + segs) * 64u);
+                    make_uint4(rb + start, rb + g1, rb + g2, ((a.b0 + own) * a.cap + segs) * kSegSlotBytes);
                 posted = true;
             }
         }
@@ -545,7 +545,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
             if (!posted) {
                 read_segment();
                 if (segs < a.cap)
-                    store_segment(((a.b0 + own) * a.cap + segs) * 64u);
+                    store_segment(((a.b0 + own) * a.cap + segs) * kSegSlotBytes);
                 else
                     spill_segment();
             }
@@ -557,7 +557,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
             for (uint32_t j = 1; j < nf; j++) {
                 read_segment();
                 if (segs < a.cap)
-                    store_segment(((a.b0 + own) * a.cap + segs) * 64u);
+                    store_segment(((a.b0 + own) * a.cap + segs) * kSegSlotBytes);
                 else
                     spill_segment();
                 s = start + 96;
@@ -608,7 +608,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
                 v[t] = *(const uint32_t*)((const char*)sm + own * R4 + s);
             }
             if (segs < a.cap) {
-                uint64_t* dst = region_ptr(a, a.b0 + own, w) + (uint64_t)segs * kSegWords;
+                uint64_t* dst = region_ptr(a, a.b0 + own, w) + (uint64_t)segs * kSegSlotWords;
 #pragma unroll
                 for (int t = 0; t < kSegWords; t++) dst[t] = pack3<SL>(v[t], v[t + 8], v[t + 16]);
                 segs++;
@@ -717,7 +717,7 @@ __global__ __launch_bounds__(kApplyBlock) void k_apply(const uint64_t* __restric
         for (uint32_t j = 0; j < nreg; j++) {
             const uint32_t r = wave + j * NWAVE;
             const uint32_t nseg = __shfl(cnt, (int)j);
-            const uint4* src = reinterpret_cast<const uint4*>(regions + ((uint64_t)r * nbins + b) * cap * kSegWords);
+            const uint4* src = reinterpret_cast<const uint4*>(regions + ((uint64_t)r * nbins + b) * cap * kSegSlotWords);
             const uint32_t n16 = nseg * (kSegWords / 2);  // 16-B pieces (2 words, 6 offsets)
             constexpr uint32_t U = LSMB_APPLY_U;           // loads in flight per lane
             for (uint32_t i0 = 0; i0 < n16; i0 += 64 * U) {
@@ -725,7 +725,8 @@ __global__ __launch_bounds__(kApplyBlock) void k_apply(const uint64_t* __restric
 #pragma unroll
                 for (uint32_t u = 0; u < U; u++) {
                     const uint32_t i = i0 + u * 64 + lane;
-                    v[u] = i < n16 ? ld_stream16(src + i) : make_uint4(0, 0, 0, 0);
+                    const uint32_t ia = kSegSlotWords == kSegWords ? i : (i / 4) * (kSegSlotWords / 2) + (i % 4);
+                    v[u] = i < n16 ? ld_stream16(src + ia) : make_uint4(0, 0, 0, 0);
                 }
 #pragma unroll
                 for (uint32_t u = 0; u < U; u++) {
@@ -1117,8 +1118,8 @@ PartitionPlan plan_partition_sl(uint32_t num_bits, uint32_t k, uint64_t n, int n
     // A region holds at most kMaxRegionSegs segments
     // a bigger plan is reported as unbounded so callers chunk the keys.
     // (and a workgroup's regions within pass A's 2^31-byte buffer range)
-    const bool fits = pl.cap_segs <= kMaxRegionSegs && (uint64_t)pl.nbins * pl.cap_segs * 64 < (1ull << 31);
-    pl.region_bytes = fits ? (uint64_t)pl.nbins * pl.grid * pl.cap_segs * 64 : ~0ull >> 2;
+    const bool fits = pl.cap_segs <= kMaxRegionSegs && (uint64_t)pl.nbins * pl.cap_segs * kSegSlotBytes < (1ull << 31);
+    pl.region_bytes = fits ? (uint64_t)pl.nbins * pl.grid * pl.cap_segs * kSegSlotBytes : ~0ull >> 2;
     pl.counts_bytes = (uint64_t)pl.nbins * pl.grid * 4;
     return pl;
 }

@@ -14,6 +14,11 @@ constexpr uint32_t kSliceWords32 = 1u << (kSliceLog2 - 5);
 constexpr uint32_t kSliceMask = (1u << kSliceLog2) - 1;
 constexpr int kSegEntries = 24;                       // 20-bit offsets per 64-B segment
 constexpr int kSegWords = 8;                          // 3 offsets per u64 word
+#ifndef LSMB_SEG_STRIDE
+#define LSMB_SEG_STRIDE 64  // bytes between a region's segments (measurement knob: 128 = one segment per line)
+#endif
+constexpr uint32_t kSegSlotBytes = LSMB_SEG_STRIDE;
+constexpr uint32_t kSegSlotWords = kSegSlotBytes / 8;
 constexpr int kBinBlock = 1024;                       // pass A workgroup
 constexpr int kApplyBlock = 1024;                     // pass B workgroup
 constexpr uint32_t kLdsFilterMaxWords32 = 40 * 1024;  // 160 KiB: whole filter in LDS
