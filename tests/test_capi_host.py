@@ -151,6 +151,32 @@ def test_degenerate_filters():
         f7.may_contain(b"x")
 
 
+def test_fresh_entry_points_reject_like_the_others():
+    # lsmb_build_*_dev_new (BloomFilterBuilder::build into output-only words):
+    # argument checks before any device work, so they run without a GPU
+    import ctypes
+    L = lsmbloom.lib()
+    vp = ctypes.c_void_p
+    nb, k = lsmbloom.params(10**8, 0.01)
+    # no context
+    assert L.lsmb_build_fixed_dev_new(None, vp(1), 16, 10, nb, k, vp(1), None) == lsmbloom.LSMB_EINVAL
+    assert L.lsmb_build_var_dev_new(None, vp(1), vp(1), 10, nb, k, vp(1), None) == lsmbloom.LSMB_EINVAL
+    assert L.lsmb_build_fixed_dev_sweep_new(None, vp(1), 16, 10, nb, k, vp(1), 0, None) == lsmbloom.LSMB_EINVAL
+    fake = vp(0x1000)  # never dereferenced: every call below fails its checks first
+    # num_bits == 0 with k > 0: the reference panics (% by zero, mod.rs:195)
+    assert L.lsmb_build_fixed_dev_new(fake, vp(1), 16, 10, 0, 7, vp(1), None) == lsmbloom.LSMB_EINVAL
+    # output words are required even for n == 0 (new() writes them)
+    assert L.lsmb_build_fixed_dev_new(fake, None, 16, 0, nb, k, None, None) == lsmbloom.LSMB_EINVAL
+    # keys are required for n > 0
+    assert L.lsmb_build_var_dev_new(fake, vp(1), None, 10, nb, k, vp(1), None) == lsmbloom.LSMB_EINVAL
+    # sweep out of range
+    n = 125_000_000
+    nb5, k5 = lsmbloom.params(10**9, 0.01)
+    assert lsmbloom.build_sweeps(nb5, n, k5) == 2
+    assert L.lsmb_build_fixed_dev_sweep_new(fake, vp(1), 16, n, nb5, k5, vp(1), 2, None) == lsmbloom.LSMB_EINVAL
+    assert L.lsmb_build_fixed_dev_sweep_new(fake, vp(1), 16, n, nb5, k5, vp(1), -1, None) == lsmbloom.LSMB_EINVAL
+
+
 @pytest.mark.skipif(_has_gpu(), reason="checks the no-device behaviour")
 def test_batched_path_fails_loudly_without_gpu():
     with pytest.raises(lsmbloom.LsmbError) as ei:
