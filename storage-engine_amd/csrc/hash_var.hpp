@@ -130,10 +130,13 @@ void k_hash_var(const uint8_t* __restrict__ d, const uint64_t* __restrict__ o, u
     // lane assignment by length class (a counting sort of the block's keys)
     uint32_t cls = 15;
     const uint64_t kbase = o[i0];
+    // (a block spanning 4 GiB or more — keys of 16 MiB on average — reads its
+    // offsets from global memory again instead)
+    const bool use_rel = LSMB_HV_REL && o[i0 + m] - kbase <= 0xFFFFFFFFull;  // block-uniform
     if (t < m) {
         const uint64_t a = o[i0 + t], b = o[i0 + t + 1];
         cls = MODE == 2 ? 0 : len_class(b - a);  // MODE 2 (microbenchmark): no sort
-        if (LSMB_HV_REL) {
+        if (use_rel) {
             rel[t] = (uint32_t)(a - kbase);
             if (t == m - 1) rel[m] = (uint32_t)(b - kbase);
         }
@@ -149,7 +152,7 @@ void k_hash_var(const uint8_t* __restrict__ d, const uint64_t* __restrict__ o, u
     const uint32_t j = perm[t];  // the key this lane hashes
     uint64_t ka = 0, kb = 0;
     if (j < m) {
-        if (LSMB_HV_REL) {  // (written before the perm barrier)
+        if (use_rel) {  // (written before the perm barrier)
             ka = kbase + rel[j];
             kb = kbase + rel[j + 1];
         } else {
