@@ -824,10 +824,13 @@ void set_max_lds(const void* fn) {
 #ifndef LSMB_HV_WIN
 #define LSMB_HV_WIN (36 * 1024)
 #endif
+#ifndef LSMB_HV_WPE
+#define LSMB_HV_WPE 0
+#endif
 template <class Out>
 void launch_hash_var(const VarLen& src, uint64_t n, Out out, hipStream_t st) {
     const uint64_t g = (n + LSMB_HV_KEYS - 1) / LSMB_HV_KEYS;
-    k_hash_var<0, LSMB_HV_KEYS, LSMB_HV_WIN, 0, Out><<<dim3((uint32_t)g), dim3(LSMB_HV_KEYS), 0, st>>>(src.d, src.o, n, out);
+    k_hash_var<0, LSMB_HV_KEYS, LSMB_HV_WIN, LSMB_HV_WPE, Out><<<dim3((uint32_t)g), dim3(LSMB_HV_KEYS), 0, st>>>(src.d, src.o, n, out);
 }
 
 template <class Src>
