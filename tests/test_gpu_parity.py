@@ -254,6 +254,35 @@ def test_build_var_c4_10m_exact(ctx, oracle):
     assert np.array_equal(words.cpu().numpy().view(np.uint64), ref)
 
 
+def test_build_var_offsets_past_4gib(ctx, oracle):
+    """Key data past 4 GiB at a small key count: 4 100 keys of 1 MiB (each
+    longer than k_hash_var's LDS window, so each is hashed from global memory
+    by its lane), then 100 k C4-shaped keys whose offsets all exceed 2^32 (the
+    offsets' high dwords are nonzero: C4's 13.2 GB has them, the 10 M-key test's
+    1.3 GB does not).  Partition build into new(1e8, 0.01) vs the oracle."""
+    import torch
+    dev = torch.device("cuda:0")
+    big, small = 4100, 100_000
+    rng = np.random.default_rng(0x4617)
+    lens = np.concatenate([np.full(big, 1 << 20, np.uint64),
+                           rng.integers(8, 257, size=small).astype(np.uint64)])
+    offs = np.zeros(big + small + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    total = int(offs[-1])
+    assert int(offs[big]) > 2**32
+    data_d = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev)
+    offs_d = torch.from_numpy(offs.view(np.int64)).to(dev)
+    n = big + small
+    nb, k = lsmbloom.params(100_000_000, 0.01)
+    words = torch.zeros(lsmbloom.num_words(nb), dtype=torch.int64, device=dev)
+    ctx.build_var_dev(data_d, offs_d, n, nb, k, words)
+    got = words.cpu().numpy().view(np.uint64)
+    data = data_d.cpu().numpy()
+    del data_d
+    ref = oracle.build_var_mt(data, offs, nb, k, 16)
+    assert np.array_equal(got, ref)
+
+
 @pytest.mark.parametrize("k", [1, 2, 7, 8, 9, 16, 17, 32, 33, 40])
 def test_build_any_k(ctx, oracle, k):
     n = 200_000
