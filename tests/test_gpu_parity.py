@@ -255,24 +255,27 @@ def test_build_var_c4_10m_exact(ctx, oracle):
 
 
 def test_build_var_offsets_past_4gib(ctx, oracle):
-    """Key data past 4 GiB at a small key count: 4 100 keys of 1 MiB (each
-    longer than k_hash_var's LDS window, so each is hashed from global memory
-    by its lane), then 100 k C4-shaped keys whose offsets all exceed 2^32 (the
-    offsets' high dwords are nonzero: C4's 13.2 GB has them, the 10 M-key test's
-    1.3 GB does not).  Partition build into new(1e8, 0.01) vs the oracle."""
+    """Key data past 2 and 4 GiB with more blocks than k_hash_var's resident
+    workgroups: 2 100 keys of 1 MiB, 300 k C4-shaped keys (offsets in
+    [2^31, 2^32): the offsets' low dwords have bit 31 set), 2 100 more 1 MiB
+    keys, 100 k C4-shaped keys (offsets above 2^32).  The 1 MiB keys are
+    longer than the LDS window, so each is hashed from global memory by its
+    lane.  ~1 580 blocks of 256 keys: more than 4 workgroups x 256 CUs, so
+    blocks past the first 1 024 are reached through a workgroup's block loop
+    in a grid-capped launch.  Partition build into new(1e8, 0.01) vs the oracle."""
     import torch
     dev = torch.device("cuda:0")
-    big, small = 4100, 100_000
     rng = np.random.default_rng(0x4617)
-    lens = np.concatenate([np.full(big, 1 << 20, np.uint64),
-                           rng.integers(8, 257, size=small).astype(np.uint64)])
-    offs = np.zeros(big + small + 1, np.uint64)
+    mib = lambda c: np.full(c, 1 << 20, np.uint64)
+    small = lambda c: rng.integers(8, 257, size=c).astype(np.uint64)
+    lens = np.concatenate([mib(2100), small(300_000), mib(2100), small(100_000)])
+    offs = np.zeros(lens.size + 1, np.uint64)
     offs[1:] = np.cumsum(lens)
     total = int(offs[-1])
-    assert int(offs[big]) > 2**32
+    assert 2**31 < int(offs[2100]) < int(offs[302_100]) < 2**32 < int(offs[304_200])
     data_d = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev)
     offs_d = torch.from_numpy(offs.view(np.int64)).to(dev)
-    n = big + small
+    n = lens.size
     nb, k = lsmbloom.params(100_000_000, 0.01)
     words = torch.zeros(lsmbloom.num_words(nb), dtype=torch.int64, device=dev)
     ctx.build_var_dev(data_d, offs_d, n, nb, k, words)
