@@ -499,7 +499,7 @@ def main():
         if tr["fresh"]:
             out["roofline"]["traffic"] = tr["bytes"]
             if tr.get("valu_insts"):
-                out["roofline"]["secondary"] = valu_roofline(tr, out["roofline"]["kernel_ms"], npg)
+                out["roofline"]["secondary"] = valu_roofline(tr, out["roofline"]["kernel_ms"], npg, nb)
         else:
             out["roofline"]["traffic_stale"] = "kernel sources changed since %s was profiled" % tr["source"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -794,7 +794,7 @@ VALU_PEAK_WAVE_INSTS = 256 * 4 * 2.4e9 / 2
 HASH_WALK_FLOOR_MS_PER_1E8 = 0.47
 
 
-def valu_roofline(tr, kernel_ms, n):
+def valu_roofline(tr, kernel_ms, n, num_bits):
     """roofline.secondary: the build's VALU work against the VALU issue
     ceiling, from the committed PMC profile's SQ_INSTS_VALU (whole-chip wave64
     VALU instructions per build).  Quarter-rate instructions (the 64-bit
@@ -809,7 +809,7 @@ def valu_roofline(tr, kernel_ms, n):
             "valu_issue_floor_ms": round(insts / VALU_PEAK_WAVE_INSTS * 1e3, 4),
             "hash_walk_floor_ms": round(HASH_WALK_FLOOR_MS_PER_1E8 * n / 1e8, 4),
             "hash_walk_floor_frac_of_hbm_roofline": round(
-                (16 * n + 8 * ((956715292 + 63) // 64)) / (HASH_WALK_FLOOR_MS_PER_1E8 * n / 1e8 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                (16 * n + 8 * ((num_bits + 63) // 64)) / (HASH_WALK_FLOOR_MS_PER_1E8 * n / 1e8 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "source": tr["source"]}
 
 

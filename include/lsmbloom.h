@@ -205,7 +205,13 @@ int lsmb_build_var_dev(lsmb_ctx* ctx, const void* d_data, const void* d_offsets,
  * BloomFilter::new (src/bloom/mod.rs:38-67) + insert of every key.  Unlike the
  * entry points above, `d_words` is OUTPUT-ONLY — its old contents are ignored,
  * every word of the filter is written — so the build needs no zeroing pass and
- * never reads the old words.  n == 0 or num_hashes == 0 writes all-zero words. */
+ * never reads the old words.  n == 0 or num_hashes == 0 writes all-zero words.
+ * Memory: a partitioned k = 7 build also allocates, once per context and kept
+ * until lsmb_close, an overflow bitmap as large as the filter (C2: 120 MB; the
+ * 2^32-1-bit C5 filter: 512 MiB), 4 bytes per 2^20 filter bits of unit marks,
+ * and 64 KiB of overflow lists per pass A workgroup per sweep (C2 and C5: 32
+ * MiB).  These are outside LSMB_WORKSPACE_MB, which bounds only the partition
+ * regions (the key chunk size follows from it). */
 int lsmb_build_fixed_dev_new(lsmb_ctx* ctx, const void* d_keys, uint32_t key_len, uint64_t n,
                              uint32_t num_bits, uint32_t num_hashes, void* d_words, void* stream);
 int lsmb_build_var_dev_new(lsmb_ctx* ctx, const void* d_data, const void* d_offsets, uint64_t n,

@@ -9,55 +9,33 @@
 #include <vector>
 
 #include "../../include/lsmbloom.h"
+#include "growbuf.hpp"
 #include "kernels.hpp"
 
 namespace lsmb {
 
-// A grow-only device buffer.
-//
-// Growing never frees: ROCm's hipFree (and hipHostFree) waits for every stream
-// of the device, so a free on the build path would stall every other context
-// (a flush next to a background compaction, src/compaction/scheduler.rs:37).
-// An outgrown buffer is retired instead — kernels queued on other streams may
-// still read it — and freed by release() at teardown (lsmb_close and the
-// handles' close functions, after their streams are synchronised).  Growth is
-// at least 1.5x, so the retired buffers never add up to more than twice the
-// live one.  Only when the device is out of memory are the retired buffers
-// freed early (a device-wide wait, but no failure).
-struct DevBuf {
-    void* p = nullptr;
-    size_t bytes = 0;
-    std::vector<void*> retired;
-    hipError_t ensure(size_t want) {
-        if (want <= bytes) return hipSuccess;
-        size_t cap = std::max(want, bytes + bytes / 2);
+// A grow-only device buffer: GrowBuf's policy (growbuf.hpp) over hipMalloc.
+// Outgrown buffers are retired, not freed, and freed by release() at teardown
+// (lsmb_close and the handles' close functions, after their streams are
+// synchronised); out of memory, the retired and then the live buffer are freed
+// before the last try.
+struct HipAlloc {
+    hipError_t last = hipSuccess;
+    void* alloc(size_t n) {
         void* q = nullptr;
-        hipError_t e = hipMalloc(&q, cap);
-        if (e != hipSuccess) {
+        last = hipMalloc(&q, n);
+        if (last != hipSuccess) {
             (void)hipGetLastError();
-            cap = want;
-            e = hipMalloc(&q, cap);
+            return nullptr;
         }
-        if (e != hipSuccess && !retired.empty()) {  // out of memory: free what no longer grows
-            (void)hipGetLastError();
-            free_retired();
-            e = hipMalloc(&q, cap);
-        }
-        if (e != hipSuccess) return e;
-        if (p) retired.push_back(p);
-        p = q;
-        bytes = cap;
-        return hipSuccess;
+        return q;
     }
-    void free_retired() {
-        for (void* r : retired) (void)hipFree(r);  // teardown / out-of-memory only
-        retired.clear();
-    }
-    void release() {
-        free_retired();
-        if (p) (void)hipFree(p);  // teardown
-        p = nullptr;
-        bytes = 0;
+    void free(void* q) { (void)hipFree(q); }  // teardown / out-of-memory only
+};
+struct DevBuf : GrowBuf<HipAlloc> {
+    hipError_t ensure(size_t want) {
+        if (GrowBuf<HipAlloc>::ensure(want)) return hipSuccess;
+        return al.last != hipSuccess ? al.last : hipErrorOutOfMemory;
     }
 };
 

@@ -142,6 +142,12 @@ void k_hash_var(const uint8_t* __restrict__ d, const uint64_t* __restrict__ o, u
         }
     }
     if (t < 16) cls_cnt[t] = 0;
+    // Every wave's window DMA has landed before any wave reads the window.  A
+    // wave of a partial last block with no key (t >= m for all its lanes) may
+    // still issue pieces and then has no later global load it waits on; the
+    // workgroup barrier alone does not order its DMA (non-tgsplit mode).
+    // Waves with keys waited on their offset loads anyway.
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const uint32_t rank = atomicAdd(&cls_cnt[cls], 1u);
     __syncthreads();

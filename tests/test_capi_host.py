@@ -206,7 +206,9 @@ def test_no_free_on_the_build_path():
     of the device, so a buffer that grows mid-run must not be freed (DevBuf and
     PinnedPool retire it until teardown).  Every free in the library sits in a
     teardown path, marked `// teardown` on its line, and the growth paths
-    (DevBuf::ensure, the pinned staging of host builds and streams) retire."""
+    (DevBuf::ensure = GrowBuf::ensure, the pinned staging of host builds and
+    streams) retire; GrowBuf frees the live buffer only out of memory
+    (tests/test_growbuf.py)."""
     import glob
     srcs = glob.glob(os.path.join(ROOT, "storage-engine_amd", "csrc", "*.hip")) + \
         glob.glob(os.path.join(ROOT, "storage-engine_amd", "csrc", "*.hpp"))
@@ -218,9 +220,15 @@ def test_no_free_on_the_build_path():
                 n += 1
                 assert "// teardown" in line, "%s:%d frees outside a teardown path: %s" % (path, no, line.strip())
     assert n > 0
+    gb = open(os.path.join(ROOT, "storage-engine_amd", "csrc", "growbuf.hpp")).read()
+    ensure = gb[gb.index("bool ensure(size_t want)"):gb.index("void free_retired()")]
+    # the only frees in ensure: the retired buffers, then the live one, each
+    # after a failed allocation
+    assert "retired.push_back(p)" in ensure
+    assert ensure.count("al.free(") == 1 and "if (!q && p) {" in ensure
+    assert ensure.count("free_retired()") == 1 and "if (!q && !retired.empty()) {" in ensure
     ctx = open(os.path.join(ROOT, "storage-engine_amd", "csrc", "ctx.hpp")).read()
-    ensure = ctx[ctx.index("hipError_t ensure(size_t want)"):ctx.index("void free_retired()")]
-    assert "retired.push_back(p)" in ensure and "hipFree" not in ensure.replace("free_retired()", "")
+    assert "struct DevBuf : GrowBuf<HipAlloc>" in ctx
 
 
 def test_sweep_ranges_tile_the_filter():

@@ -229,6 +229,25 @@ def test_build_var_every_length_class(ctx, oracle):
         _cmp(ctx.build_var(blob, offs, nb, k), oracle.build_var(blob, offs, nb, k))
 
 
+@pytest.mark.parametrize("tail", [1, 40, 64])
+def test_build_var_partial_last_block(ctx, oracle, tail):
+    """A last k_hash_var block of <= 64 keys that hold more than 1 KiB: the
+    block's waves 1-3 have no key but still issue window pieces (LDS-DMA),
+    which wave 0's lanes then read.  256 k + tail keys, the tail
+    keys 200-256 B long, partition build (the k_hash_var path) vs the oracle."""
+    rng = np.random.default_rng(0x7A11 + tail)
+    n = 256 * 1000 + tail
+    lens = rng.integers(8, 257, size=n).astype(np.uint64)
+    lens[-tail:] = rng.integers(200, 257, size=tail)
+    assert int(lens[-tail:].sum()) > 1024 or tail == 1
+    offs = np.zeros(n + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    blob = keygen.stream_bytes(0x7A11 + tail, int(offs[-1]))
+    nb, k = lsmbloom.params(10_000_000, 0.01)
+    assert lsmbloom.build_strategy(nb, n, k) == "partition"
+    _cmp(ctx.build_var(blob, offs, nb, k), oracle.build_var(blob, offs, nb, k))
+
+
 def test_build_var_c4_shape(ctx, oracle):
     n = 1_000_000
     data, offs = keygen.varlen(n)
