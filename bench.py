@@ -43,7 +43,9 @@ def parse():
                     help="keys of the whole run, split over the ranks (default: 1e8 = C2 at N=1, 1e9 = C5 at N>1)")
     ap.add_argument("--keys-per-gpu", type=int, default=0,
                     help="weak scaling instead: this many keys per rank (overrides --global-keys)")
-    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
+    ap.add_argument("--backend", default="nccl",
+                    help="N>1 merge: nccl (RCCL collectives), gloo (host-staged), ipc (peer loads over IPC-mapped "
+                         "device words, gloo barriers)")
     ap.add_argument("--probe-keys", type=int, default=10_000_000)
     ap.add_argument("--probe-filters", type=int, default=8)
     ap.add_argument("--no-probe", action="store_true")
@@ -256,8 +258,8 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(args.backend)
+        else:  # gloo; ipc: gloo orders the phases, the words move by peer loads
+            dist.init_process_group("gloo" if args.backend == "ipc" else args.backend)
     ctx = lsmbloom.Context(dev.index)
     # One explicit stream for all of this rank's work: on torch's default (the
     # legacy null) stream, the library maps stream NULL to its context's
@@ -297,8 +299,14 @@ def main():
         else:
             ctx.build_fixed_dev_new(keys, 16, npg, nb, k, words)
 
+    # --backend ipc: the merge by peer loads over IPC-mapped words (no
+    # collective library on the data path; lsmbloom.dist.IpcMerge)
+    ipc = ldist.IpcMerge(words, ctx) if world > 1 and args.backend == "ipc" else None
+
     def allreduce():
-        if world > 1:
+        if ipc:
+            ipc.allreduce()
+        elif world > 1:
             ldist.or_allreduce_(words, ctx=ctx)
 
     # N > 1 step: the partitioned build runs in sweeps (C5: 2 x 256 MiB word
@@ -316,6 +324,15 @@ def main():
             allreduce()
             return
         main = torch.cuda.current_stream(dev)
+        if ipc:  # every sweep queued first: the host waits per range while the next sweep builds
+            for s in range(nsw):
+                ctx.build_fixed_dev_sweep_new(keys, 16, npg, nb, k, words, s)
+                sweep_ev[s].record(main)
+            for s, (a, b) in enumerate(ranges):
+                side.wait_event(sweep_ev[s])
+                ipc.allreduce(a, b, stream=side)
+            main.wait_stream(side)
+            return
         for s, (a, b) in enumerate(ranges):
             ctx.build_fixed_dev_sweep_new(keys, 16, npg, nb, k, words, s)
             sweep_ev[s].record(main)
@@ -425,8 +442,11 @@ def main():
         out["config"]["backend"] = args.backend
         out["step_split"] = {"build_ms": round(build_ms, 4), "or_allreduce_ms": round(coll_ms, 4),
                              "what": "serial steps (untimed pass), slowest rank: device build (fresh) / "
-                                     "bitwise-OR allreduce (all_to_all reduce-scatter + native OR kernel "
-                                     "+ all_gather) of the whole filter",
+                                     + ("bitwise-OR allreduce by peer loads over IPC-mapped words (OR gather "
+                                        "reduce-scatter + copy all-gather, host barriers between phases)"
+                                        if ipc else
+                                        "bitwise-OR allreduce (all_to_all reduce-scatter + native OR kernel "
+                                        "+ all_gather)") + " of the whole filter",
                              "serial_ms_per_step": round(serial_ms, 4),
                              "overlap_calibration": calib,
                              "timed_step": ("%d build sweeps, each sweep's word range OR-allreduced on a side "
@@ -507,6 +527,8 @@ def main():
         out["cpu_baseline"]["gpu_over_cpu_1thread"] = round(value / out["cpu_baseline"]["value"], 1)
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if ipc:
+        ipc.close()
     ctx.close()
     if world > 1:
         dist.destroy_process_group()

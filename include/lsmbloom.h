@@ -319,6 +319,38 @@ int lsmb_multi_build_block(lsmb_multi* m, const uint8_t* data, const uint64_t* o
  * (slowest shard), [2] merge = [0] - [1]. */
 int lsmb_multi_last_ms(lsmb_multi* m, float* out3);
 
+/* ---- one process per GPU: cross-process peer-load merge ------------------- */
+/* The same OR merge between processes (one per GPU, e.g. torch.distributed
+ * ranks), without a collective library: every rank exports the device
+ * allocation holding its partial words, maps the other ranks' allocations
+ * (over xGMI when they sit on other GPUs of the node; the same HBM when they
+ * share one), and merges with peer loads: rank g ORs word-slice g of every
+ * partial into its own words (lsmb_or_gather_dev with all G sources), then
+ * copies every other merged slice from its owner (one source each).  The
+ * caller orders the ranks between the phases (a host barrier after each
+ * rank's stream has finished).  Replaces what RCCL cannot do in one call (it
+ * has no bitwise-OR reduction) for the sharded flush / compaction of
+ * src/db/mod.rs:377-383 and src/compaction/scheduler.rs:150-158. */
+#define LSMB_IPC_HANDLE_BYTES 64
+
+/* Handle of the device allocation holding d_ptr (hipIpcGetMemHandle) and
+ * d_ptr's byte offset in it. */
+int lsmb_ipc_export(const void* d_ptr, uint8_t* handle, uint64_t* offset);
+
+/* Maps another process's allocation into this context's device
+ * (hipIpcOpenMemHandle, peer access enabled lazily); *d_base = its first
+ * byte here.  A handle exported by this same process is LSMB_EINVAL. */
+int lsmb_ipc_import(lsmb_ctx* ctx, const uint8_t* handle, void** d_base);
+
+/* Unmaps an allocation lsmb_ipc_import mapped (d_base as returned). */
+int lsmb_ipc_close(lsmb_ctx* ctx, void* d_base);
+
+/* d_dst[i] = OR over j < nsrc of d_srcs[j][i], i < nwords (u64 words; any
+ * source may be d_dst itself, or mapped peer memory).  Asynchronous on
+ * `stream`.  nsrc == 1 is a copy; 1 <= nsrc <= 16. */
+int lsmb_or_gather_dev(lsmb_ctx* ctx, void* d_dst, const void* const* d_srcs, uint32_t nsrc, uint64_t nwords,
+                       void* stream);
+
 /* ---- device-resident filter sets (multi-get pre-check) --------------------- */
 /* An lsmb_fset keeps up to 64 SSTable filters resident in device memory, each
  * with its table's key range [min_key, max_key] (SSTable meta,

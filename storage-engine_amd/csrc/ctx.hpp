@@ -130,6 +130,9 @@ struct lsmb_ctx {
 
 namespace lsmb {
 
+// `stream` of an entry point, NULL = the context's own build stream.
+hipStream_t pick_stream(lsmb_ctx* c, void* stream);
+
 // Device build of one batch on `st` into d_words (OR-accumulate; fresh =
 // BloomFilter::new + inserts: d_words is output-only), chunked so the
 // partition workspace stays bounded.  Asynchronous.

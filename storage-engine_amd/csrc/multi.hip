@@ -384,6 +384,62 @@ int lsmb_multi_build_block(lsmb_multi* m, const uint8_t* data, const uint64_t* o
     return rc;
 }
 
+// ---- one process per GPU: IPC mappings + the peer-load OR gather
+int lsmb_ipc_export(const void* d_ptr, uint8_t* handle, uint64_t* offset) {
+    if (!d_ptr || !handle || !offset) return fail(LSMB_EINVAL, "null argument");
+    static_assert(sizeof(hipIpcMemHandle_t) == LSMB_IPC_HANDLE_BYTES, "IPC handle size");
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    HIP_TRY(hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)d_ptr));
+    hipIpcMemHandle_t h;
+    HIP_TRY(hipIpcGetMemHandle(&h, (void*)base));
+    memcpy(handle, &h, sizeof h);
+    *offset = (uint64_t)((const char*)d_ptr - (const char*)base);
+    return LSMB_OK;
+}
+
+int lsmb_ipc_import(lsmb_ctx* c, const uint8_t* handle, void** d_base) {
+    if (!c || !handle || !d_base) return fail(LSMB_EINVAL, "null argument");
+    *d_base = nullptr;
+    DevGuard g(c->dev);
+    hipIpcMemHandle_t h;
+    memcpy(&h, handle, sizeof h);
+    const hipError_t e = hipIpcOpenMemHandle(d_base, h, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        *d_base = nullptr;
+        return fail(e == hipErrorInvalidContext || e == hipErrorInvalidValue ? LSMB_EINVAL : LSMB_EHIP,
+                    "hipIpcOpenMemHandle: %s (a handle of this same process cannot be opened)", hipGetErrorString(e));
+    }
+    return LSMB_OK;
+}
+
+int lsmb_ipc_close(lsmb_ctx* c, void* d_base) {
+    if (!c || !d_base) return fail(LSMB_EINVAL, "null argument");
+    DevGuard g(c->dev);
+    HIP_TRY(hipIpcCloseMemHandle(d_base));  // teardown of a mapping, no device memory freed
+    return LSMB_OK;
+}
+
+int lsmb_or_gather_dev(lsmb_ctx* c, void* d_dst, const void* const* d_srcs, uint32_t nsrc, uint64_t nwords,
+                       void* stream) {
+    if (!c || !d_srcs) return fail(LSMB_EINVAL, "null argument");
+    if (nsrc < 1 || nsrc > (uint32_t)kMaxShards) return fail(LSMB_EINVAL, "nsrc must be in [1, %d]", kMaxShards);
+    if (nwords == 0) return LSMB_OK;
+    if (!d_dst) return fail(LSMB_EINVAL, "null device pointer");
+    OrSources s;
+    s.n = nsrc;
+    for (uint32_t j = 0; j < nsrc; j++) {
+        if (!d_srcs[j]) return fail(LSMB_EINVAL, "null source %u", j);
+        if (((uintptr_t)d_srcs[j] & 7) != 0) return fail(LSMB_EINVAL, "source %u is not 8-byte aligned", j);
+        s.p[j] = d_srcs[j];
+    }
+    if (((uintptr_t)d_dst & 7) != 0) return fail(LSMB_EINVAL, "d_dst is not 8-byte aligned");
+    DevGuard g(c->dev);
+    HIP_TRY(launch_or_gather((uint64_t*)d_dst, s, nwords, c->num_cus, pick_stream(c, stream)));
+    return LSMB_OK;
+}
+
 int lsmb_multi_last_ms(lsmb_multi* m, float* out3) {
     if (!m || !out3) return fail(LSMB_EINVAL, "null argument");
     if (!m->timed) return fail(LSMB_EINVAL, "no multi-GPU build on this handle");

@@ -107,6 +107,10 @@ SIGNATURES = {
     "lsmb_multi_build_block": (ctypes.c_int, [vp, u8p, u64p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
                                               ctypes.c_uint32, u8p, ctypes.c_uint64]),
     "lsmb_multi_last_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_float)]),
+    "lsmb_ipc_export": (ctypes.c_int, [vp, u8p, u64p]),
+    "lsmb_ipc_import": (ctypes.c_int, [vp, u8p, ctypes.POINTER(vp)]),
+    "lsmb_ipc_close": (ctypes.c_int, [vp, vp]),
+    "lsmb_or_gather_dev": (ctypes.c_int, [vp, vp, ctypes.POINTER(vp), ctypes.c_uint32, ctypes.c_uint64, vp]),
     "lsmb_stream_open": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(vp)]),
     "lsmb_stream_reset": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32]),
     "lsmb_stream_close": (None, [vp]),
@@ -185,6 +189,15 @@ def params(expected_items, false_positive_rate):
     nb, k = ctypes.c_uint32(), ctypes.c_uint32()
     _check(lib().lsmb_params(int(expected_items), float(false_positive_rate), ctypes.byref(nb), ctypes.byref(k)))
     return nb.value, k.value
+
+
+def ipc_export(t):
+    """(handle bytes, byte offset) of the device allocation holding tensor t's
+    storage (lsmb_ipc_export), for another process's Context.ipc_import."""
+    h = np.zeros(64, dtype=np.uint8)
+    off = ctypes.c_uint64()
+    _check(lib().lsmb_ipc_export(vp(t.data_ptr()), _p(h, u8p), ctypes.byref(off)))
+    return h.tobytes(), off.value
 
 
 def num_words(num_bits):
@@ -363,6 +376,23 @@ class Context:
     def or_reduce_dev(self, dst, src, nwords, nsrc, stride_words, stream=None):
         _check(lib().lsmb_or_reduce_dev(self.h, vp(dst.data_ptr()), vp(src.data_ptr()), nwords, nsrc,
                                         stride_words, self._stream(stream)))
+
+    def or_gather_dev(self, dst_ptr, src_ptrs, nwords, stream=None):
+        """dst[i] = OR of src_j[i] over the raw device pointers src_ptrs (own or
+        IPC-mapped peer memory), nwords u64 words (lsmb_or_gather_dev)."""
+        arr = (vp * len(src_ptrs))(*[vp(int(p)) for p in src_ptrs])
+        _check(lib().lsmb_or_gather_dev(self.h, vp(int(dst_ptr)), arr, len(src_ptrs), int(nwords),
+                                        self._stream(stream)))
+
+    def ipc_import(self, handle):
+        """Maps another process's device allocation (lsmb_ipc_import) -> base pointer (int)."""
+        h = np.frombuffer(bytes(handle), dtype=np.uint8).copy()
+        base = vp()
+        _check(lib().lsmb_ipc_import(self.h, _p(h, u8p), ctypes.byref(base)))
+        return int(base.value)
+
+    def ipc_close(self, base):
+        _check(lib().lsmb_ipc_close(self.h, vp(int(base))))
 
     def gen_key16_dev(self, seed, first, n, out, stream=None):
         _check(lib().lsmb_gen_key16_dev(self.h, seed, first, n, vp(out.data_ptr()), self._stream(stream)))

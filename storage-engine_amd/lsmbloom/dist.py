@@ -80,3 +80,70 @@ def or_allreduce_(words, group=None, ctx=None):
     dist.all_gather_into_tensor(out, mine, group=group)
     words.copy_(out[:n])
     return words
+
+
+class IpcMerge:
+    """The OR-allreduce by peer loads between processes (one per GPU), with no
+    collective library on the data path (include/lsmbloom.h, "cross-process
+    peer-load merge"): every rank exports the device allocation holding its
+    words once, maps every other rank's (lsmb_ipc_import: xGMI peer mappings
+    across GPUs, the same HBM when ranks share one), and merges a word range
+    in two peer-load kernels:
+      1. reduce-scatter: rank g ORs word-slice g of all G partials into its own
+         words (one lsmb_or_gather_dev, G sources);
+      2. all-gather: rank g copies every other merged slice from its owner.
+    `group` (gloo) only orders the phases: a host barrier after each rank's
+    stream finished the previous phase, and one at the end so that no rank
+    rewrites its words while a peer may still read them.  Per GPU it reads
+    (G-1)/G of the range twice over the peer links, the RCCL path's bytes."""
+
+    def __init__(self, words, ctx, group=None):
+        import lsmbloom
+        self.words, self.ctx, self.group = words, ctx, group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        h, off = lsmbloom.ipc_export(words)
+        allh = [None] * self.world
+        dist.all_gather_object(allh, (h, off, words.numel(), words.device.index), group=group)
+        self.bases, self.ptrs = [], []
+        for r, (hh, oo, n, _) in enumerate(allh):
+            if n != words.numel():
+                raise ValueError("rank %d's words hold %d words, mine %d" % (r, n, words.numel()))
+            if r == self.rank:
+                self.ptrs.append(words.data_ptr())
+            else:
+                base = ctx.ipc_import(hh)
+                self.bases.append(base)
+                self.ptrs.append(base + oo)
+
+    def close(self):
+        dist.barrier(group=self.group)  # no peer reads my words any more
+        for b in self.bases:
+            self.ctx.ipc_close(b)
+        self.bases, self.ptrs = [], []
+
+    def _phase_done(self, stream):
+        stream.synchronize()
+        dist.barrier(group=self.group)
+
+    def allreduce(self, lo=0, hi=None, stream=None):
+        """In-place OR-allreduce of words[lo:hi] (word indices) over the group.
+        The caller's pending work on `stream` (default: current) that writes
+        words[lo:hi] is waited for first; returns when every rank's range is
+        merged (host-synchronous)."""
+        hi = self.words.numel() if hi is None else hi
+        stream = stream or torch.cuda.current_stream(self.words.device)
+        self._phase_done(stream)  # every partial of the range is final
+        per = _slices(hi - lo, self.world)
+        sl = [(min(hi, lo + r * per), min(hi, lo + (r + 1) * per)) for r in range(self.world)]
+        a, b = sl[self.rank]
+        if b > a:
+            self.ctx.or_gather_dev(self.ptrs[self.rank] + 8 * a, [p + 8 * a for p in self.ptrs], b - a,
+                                   stream=stream.cuda_stream)
+        self._phase_done(stream)  # every slice merged
+        for r, (a, b) in enumerate(sl):
+            if r != self.rank and b > a:
+                self.ctx.or_gather_dev(self.ptrs[self.rank] + 8 * a, [self.ptrs[r] + 8 * a], b - a,
+                                       stream=stream.cuda_stream)
+        self._phase_done(stream)  # every rank holds the merged range; words may be rewritten
+        return self.words

@@ -253,13 +253,79 @@ def test_dist_or_allreduce_device_path(oracle, world, n, filter_n):
         assert mine == _digest(sl), "rank %d reduce-scatter slice differs" % rank
 
 
+def _ipc_worker(rank, world, port, n, filter_n, per_sweep, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, os.path.join(ROOT, "storage-engine_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch
+    import torch.distributed as dist
+
+    import lsmbloom
+    from lsmbloom import dist as ldist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda:0")
+        ctx = lsmbloom.Context(0)
+        nb, k = lsmbloom.params(filter_n, 0.01)
+        lo, hi = n * rank // world, n * (rank + 1) // world
+        keys = torch.empty((hi - lo, 16), dtype=torch.uint8, device=dev)
+        ctx.gen_key16_dev(0x5EED0001, lo, hi - lo, keys)
+        words = torch.empty(lsmbloom.num_words(nb), dtype=torch.int64, device=dev)
+        words.fill_(-1)  # garbage: the fresh build writes every word
+        m = ldist.IpcMerge(words, ctx)
+        nsw = lsmbloom.build_sweeps(nb, hi - lo, k)
+        if per_sweep:  # the bench's overlapped form: sweep s's range merged after sweep s
+            for s in range(nsw):
+                ctx.build_fixed_dev_sweep_new(keys, 16, hi - lo, nb, k, words, s)
+                a, b = lsmbloom.sweep_words(nb, hi - lo, s, k)
+                m.allreduce(a, b)
+        else:
+            ctx.build_fixed_dev_new(keys, 16, hi - lo, nb, k, words)
+            m.allreduce()
+        torch.cuda.synchronize()
+        q.put((rank, nsw, _digest(words.cpu().numpy().view(np.uint64))))
+        m.close()
+        ctx.close()
+    finally:
+        dist.destroy_process_group()
+
+
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("filter_keys", [None, 1_000_000_000])
-def test_bench_launches_its_own_ranks(filter_keys):
+@pytest.mark.parametrize("world,n,filter_n,per_sweep", [(2, 3_000_000, 30_000_000, False),
+                                                        (3, 500_001, 500_001, False),     # ragged slices
+                                                        (4, 4_000_000, 1_000_000_000, True)])  # C5's filter, 2 ranges
+def test_ipc_or_allreduce_cross_process(oracle, world, n, filter_n, per_sweep):
+    """the N > 1 merge without RCCL — `world` processes
+    on cuda:0, each exporting its words (lsmb_ipc_export), mapping the others'
+    (lsmb_ipc_import) and merging by peer loads (lsmb_or_gather_dev), the path
+    `bench.py --backend ipc` times.  RCCL refuses two ranks on one GPU; IPC
+    does not, so the cross-process product merge runs here.  Every rank's
+    merged words == the single-process oracle build (digest)."""
+    import torch.multiprocessing as mp
+    mpc = mp.get_context("spawn")
+    q = mpc.Queue()
+    port = _free_port()
+    procs = [mpc.Process(target=_ipc_worker, args=(r, world, port, n, filter_n, per_sweep, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    nb, k = lsmbloom.params(filter_n, 0.01)
+    ref = oracle.build_fixed_mt(keygen.key16(0x5EED0001, 0, n), 16, nb, k, 16)
+    for rank, nsw, words in res:
+        assert nsw == (2 if per_sweep else nsw)
+        assert words == _digest(ref), "rank %d merged filter differs" % rank
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("filter_keys,backend", [(None, "gloo"), (1_000_000_000, "gloo"), (1_000_000_000, "ipc")])
+def test_bench_launches_its_own_ranks(filter_keys, backend):
     """`python bench.py --gpus 2` (no torchrun) starts two ranks itself; here
     over gloo, both on cuda:0.  The line must say n_gpus 2, carry the split
     build / OR-allreduce timing, and the rank-0 word-for-word self-check."""
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", backend,
            "--global-keys", "8000000", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-e2e",
            "--no-varlen", "--no-exact10", "--probe-keys", "200000"]
     if filter_keys:  # C5's 2^32-1-bit filter: 2 sweeps, per-range allreduce overlapped
