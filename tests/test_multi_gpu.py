@@ -293,7 +293,7 @@ def _ipc_worker(rank, world, port, n, filter_n, per_sweep, q):
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("world,n,filter_n,per_sweep", [(2, 3_000_000, 30_000_000, False),
                                                         (3, 500_001, 500_001, False),     # ragged slices
-                                                        (4, 4_000_000, 1_000_000_000, True)])  # C5's filter, 2 ranges
+                                                        (4, 8_000_000, 1_000_000_000, True)])  # C5's filter, 2 ranges
 def test_ipc_or_allreduce_cross_process(oracle, world, n, filter_n, per_sweep):
     """the N > 1 merge without RCCL — `world` processes
     on cuda:0, each exporting its words (lsmb_ipc_export), mapping the others'
@@ -315,7 +315,7 @@ def test_ipc_or_allreduce_cross_process(oracle, world, n, filter_n, per_sweep):
     nb, k = lsmbloom.params(filter_n, 0.01)
     ref = oracle.build_fixed_mt(keygen.key16(0x5EED0001, 0, n), 16, nb, k, 16)
     for rank, nsw, words in res:
-        assert nsw == (2 if per_sweep else nsw)
+        assert nsw == 2 or not per_sweep  # 2 M keys per rank: C5's filter builds in 2 sweeps
         assert words == _digest(ref), "rank %d merged filter differs" % rank
 
 
