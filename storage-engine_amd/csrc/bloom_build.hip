@@ -263,7 +263,11 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
     static_assert(PER == 1 || EXACT, "two keys per lane: exact k only");
     constexpr uint32_t kMask = (1u << SL) - 1;
     constexpr int NP = PER * KMAX;  // positions per lane per phase
-    extern __shared__ uint32_t sm[];
+    // The whole LDS, statically: its base is then a compile-time 0, so ring,
+    // fill and job addresses need no base add (a dynamic extern array's base
+    // is a link-time symbol: one more VALU add per LDS address).  Pass A
+    // always runs one workgroup per CU with all of the LDS.
+    __shared__ uint32_t sm[kLdsBytes / 4];
     const uint32_t k = EXACT ? (uint32_t)KMAX : k_;
     const uint32_t R = a.ring, R4 = 4 * a.ring, nb = a.nb;
     uint32_t* fill = sm + (size_t)(nb + 1) * R;  // nb + 1 fill words (the last: sink)
@@ -527,7 +531,10 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
         for (uint32_t r = 0; r < kCoopRounds; r++) {
             const uint32_t j = r * 16 + (lane >> 2), l = lane & 3;
             uint32_t off = kDrop;
-            uint2 w0 = make_uint2(0, 0), w1 = make_uint2(0, 0);
+            // a lane with no job stores at a dropped offset: its data is never
+            // written, so it need not be defined (no register clears)
+            uint2 w0, w1;
+            asm("" : "=v"(w0.x), "=v"(w0.y), "=v"(w1.x), "=v"(w1.y));
             if (j < jobs) {
                 const uint4 jb = jobtab[wave * kBinJobsPerWave + j];
                 // segment word 2l+e = pack3<SL>(group0[2l+e], group1[2l+e], group2[2l+e])
@@ -953,11 +960,9 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
             a.ovl_cap = kOvfListCap;
             a.err = ws.err;
             a.nbins = pl.nbins;
-            const size_t smem = (size_t)(a.nb + 1) * (4 * a.ring + kBinExtraBytes) + kBinJobBytes;
-            auto go = [&](auto kern) {
-                set_max_lds((const void*)kern);
-                kern<<<dim3(pl.grid), dim3(kBinBlock), smem, st>>>(src, n, md, k, a);
-            };
+            // (k_bin's LDS is static, kLdsBytes; the plan's layout fits it)
+            if ((size_t)(a.nb + 1) * (4 * a.ring + kBinExtraBytes) + kBinJobBytes > kLdsBytes) return hipErrorInvalidValue;
+            auto go = [&](auto kern) { kern<<<dim3(pl.grid), dim3(kBinBlock), 0, st>>>(src, n, md, k, a); };
             const bool full = pl.sweeps == 1;
             auto go7 = [&](auto slc) {  // k = 7 (BloomFilter::new at fpr 0.01), bin width 2^SL
                 constexpr int SL = decltype(slc)::value;

@@ -29,12 +29,26 @@
 
 namespace lsmb {
 
+// f64 of y < 2^64 as hi32(y)·2^32 + lo32(y), one rounding (the fma).  On the
+// device the high word is converted with an explicit v_cvt_f64_u32: left to
+// the compiler, (double)(uint32_t)(y >> 32) is widened to a 64-bit uitofp
+// whose lowering adds a +0.0 (one more f64 add per reduction).
+LSMB_HD double f64_of_u64(uint64_t y) {
+#ifdef __HIP_DEVICE_COMPILE__
+    double hd;
+    asm("v_cvt_f64_u32 %0, %1" : "=v"(hd) : "v"((uint32_t)(y >> 32)));
+#else
+    const double hd = (double)(uint32_t)(y >> 32);
+#endif
+    return fma(hd, 4294967296.0, (double)(uint32_t)y);
+}
+
 struct Mod32 {
     uint32_t d;     // divisor (num_bits), 1 <= d < 2^32
     uint32_t t32;   // 2^32 mod d
     uint32_t t64;   // 2^64 mod d
     uint32_t dt;    // d - t64 (in (0, d])
-    double inv;     // 1.0 / d
+    double inv;     // 1/d rounded, then 4 ulps toward 0: strictly below 1/d
 
     static Mod32 make(uint32_t d32) {
         Mod32 r;
@@ -43,28 +57,41 @@ struct Mod32 {
         r.t64 = (uint32_t)((uint64_t)(((unsigned __int128)1 << 64) % d32));
         r.dt = d32 - r.t64;
         r.inv = 1.0 / (double)d32;
+        for (int i = 0; i < 4; i++) r.inv = nextafter(r.inv, 0.0);
         return r;
     }
 
+    // With inv biased low, q = trunc(f64(y) * inv) never exceeds floor(y/d)
+    // and is at most one below it: f64(y) and the product each round by at
+    // most 2^-53 relative, and inv sits between 2^-51 and 2^-49 below 1/d,
+    // so qd < y/d and y/d - qd < 2^32 * 2^-48.  So y - q*d lies in [0, 2d).
     LSMB_HD uint32_t reduce(uint64_t x) const {
         const uint64_t y = (uint64_t)(uint32_t)(x >> 32) * t32 + (uint32_t)x;
-        const double yd = fma((double)(uint32_t)(y >> 32), 4294967296.0, (double)(uint32_t)y);
-        const double qd = yd * inv;
-        const uint32_t q = qd >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)qd;
-        int64_t r = (int64_t)(y - (uint64_t)q * d);
-        if (r < 0) r += d;
-        if (r >= (int64_t)d) r -= d;
+        const uint32_t q = (uint32_t)(f64_of_u64(y) * inv);  // < y/d < 2^32
+        uint64_t r = y - (uint64_t)q * d;
+        if (r >= d) r -= d;
         return (uint32_t)r;
+    }
+    // The same for d <= 2^31 (Walk32's domain): r < 2d <= 2^32 fits a u32, so
+    // the remainder is one 32-bit multiply-subtract and one conditional
+    // subtract (an unsigned min): 10 VALU instructions against 19.
+    LSMB_HD uint32_t reduce31(uint64_t x) const {
+        const uint64_t y = (uint64_t)(uint32_t)(x >> 32) * t32 + (uint32_t)x;
+        const uint32_t q = (uint32_t)(f64_of_u64(y) * inv);
+        const uint32_t r = (uint32_t)y - q * d;  // y - q d mod 2^32, exact: in [0, 2d)
+        const uint32_t s = r - d;
+        return s < r ? s : r;
     }
 };
 
 // The same reduction for small moduli, d < 2^14 (SST-sized filters: the
 // store's new(1000, 0.01) is 9 568 bits).  x's four 16-bit limbs times
-// t_j = 2^(16 j) mod d sum to y < 2^16 + 3·2^16·d < 2^32, so y/d < 2^18 + 1;
-// one f32 estimate q = trunc(f32(y)·f32(1/d)) is then within 1 of floor(y/d)
-// (f32(y) is off by < y·2^-24, i.e. < 0.02 after the division, and the two
-// other roundings by < 2^18·2^-23), and one fix-up each way finishes it.
-// Full-rate 24-bit multiplies and f32 only: no 64-bit products, no f64.
+// t_j = 2^(16 j) mod d sum to y < 2^16 + 3·2^16·d < 2^32, so y/d < 2^18.
+// inv is 1/d rounded to f32 and stepped 4 ulps toward 0 (3 to 9 · 2^-24
+// below 1/d), so q = trunc(f32(y)·inv) is below y/d (the two roundings add at
+// most 2·2^-24) and above y/d - 2^18·11·2^-24: q is floor(y/d) or one less,
+// and one conditional subtract finishes it.  24-bit multiplies and f32 only:
+// no 64-bit products, no f64.
 struct Mod14 {
     uint32_t d, t16, t32, t48;  // 2^(16 j) mod d
     uint32_t t64, dt;           // 2^64 mod d, d - t64 (the walk's carry step)
@@ -79,6 +106,7 @@ struct Mod14 {
         r.t64 = (uint32_t)((uint64_t)(((unsigned __int128)1 << 64) % d32));
         r.dt = d32 - r.t64;
         r.inv = 1.0f / (float)d32;
+        for (int i = 0; i < 4; i++) r.inv = nextafterf(r.inv, 0.0f);
         return r;
     }
     static LSMB_HD bool fits(uint32_t d) { return d >= 1 && d < (1u << 14); }
@@ -96,12 +124,11 @@ struct Mod14 {
         const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
         const uint32_t y = (lo & 0xFFFFu) + mul24(lo >> 16, t16) + mul24(hi & 0xFFFFu, t32) + mul24(hi >> 16, t48);
         const uint32_t q = (uint32_t)((float)y * inv);
-        uint32_t r = y - mul24(q, d);  // in [-d, 2d), wrapped (q < 2^19, d < 2^14)
-        const uint32_t a = r + d;
-        r = a < r ? a : r;       // q one too high: r wrapped below 0
+        const uint32_t r = y - mul24(q, d);  // in [0, 2d) (q < 2^18, d < 2^14)
         const uint32_t b = r - d;
-        return b < r ? b : r;    // q one too low: r in [d, 2d)
+        return b < r ? b : r;
     }
+    LSMB_HD uint32_t reduce31(uint64_t x) const { return reduce(x); }
 };
 
 // k positions of one key, i = 0, 1, ..., for d <= 2^31 (all sums fit 32 bits).
@@ -117,8 +144,8 @@ struct Walk32T {
     uint32_t r, s0, s1, d;
 
     LSMB_HD Walk32T(const M& md, uint64_t h1, uint64_t h2_) : x(h1), h2(h2_), d(md.d) {
-        r = md.reduce(h1);
-        s0 = md.reduce(h2_);
+        r = md.reduce31(h1);
+        s0 = md.reduce31(h2_);
         const uint32_t t = s0 + md.dt;  // < 2d <= 2^32
         s1 = t - md.d < t ? t - md.d : t;
     }

@@ -32,6 +32,8 @@
 namespace lsmb {
 namespace {
 
+constexpr uint32_t kProbeTableBytes = 64 * 1024;  // bit-sliced tables: the launchers' LDS cap
+
 using ks::Fixed16;
 using ks::FixedN;
 using ks::VarLen;
@@ -59,7 +61,14 @@ __global__ __launch_bounds__(BS) void k_probe_sliced(Src src, uint64_t n, typena
                                                       const ProbeFilter* __restrict__ filters,
                                                       uint32_t nfilt, uint32_t stride,
                                                       uint8_t* __restrict__ out) {
-    extern __shared__ __align__(16) uint8_t smem_raw[];
+    // 1024-thread instantiations (the hot 16-B-key / k = 7 ones) hold the
+    // table in static LDS of the 64 KiB maximum: a static array's base is a
+    // compile-time 0, so a table read is one ds_read at the position itself
+    // (a dynamic extern array's base is a link-time symbol: one more VALU add
+    // per read, 7 per key).  Two such workgroups still fit a CU.
+    extern __shared__ __align__(16) uint8_t smem_dyn[];
+    __shared__ __align__(16) uint8_t smem_stat[BS == 1024 ? kProbeTableBytes : 16];
+    uint8_t* const smem_raw = BS == 1024 ? smem_stat : smem_dyn;
     T* table = reinterpret_cast<T*>(smem_raw);
     const uint32_t nw32 = (uint32_t)(((uint64_t)num_bits + 31) / 32);  // 64-bit: num_bits may be 2^32-1
     // The filters' word pointers and output bits, loaded once and all at
@@ -320,7 +329,10 @@ template <class Src, typename T, int K, int BS = 256, class W = Walk32>
 __global__ __launch_bounds__(BS) void k_fset_sliced(Src src, uint64_t n, const RangedFilter* __restrict__ filters,
                                                      uint32_t nfilt, FsetRanges rg, uint32_t k_,
                                                      typename W::Mod md, uint64_t* __restrict__ out) {
-    extern __shared__ __align__(16) uint8_t smem_raw[];
+    // static table for the 1024-thread instantiations, as in k_probe_sliced
+    extern __shared__ __align__(16) uint8_t smem_dyn[];
+    __shared__ __align__(16) uint8_t smem_stat[BS == 1024 ? kProbeTableBytes : 16];
+    uint8_t* const smem_raw = BS == 1024 ? smem_stat : smem_dyn;
     __shared__ RangedFilter fl[64];
     __shared__ FsetLds L;
     T* table = reinterpret_cast<T*>(smem_raw);
@@ -544,13 +556,14 @@ hipError_t fset_probe_with(const Src& src, uint64_t n, const RangedFilter* df, u
     if (shared_nb > 0 && shared_k > 0) {
         const size_t tsz = nfilt <= 8 ? 1 : nfilt <= 16 ? 2 : nfilt <= 32 ? 4 : 8;
         const size_t smem = (size_t)(((uint64_t)shared_nb + 31) / 32) * 32 * tsz;
-        if (smem <= 64 * 1024) {
+        if (smem <= kProbeTableBytes) {
             const Mod32 m32 = Mod32::make(shared_nb);
             auto go = [&](auto kern, auto md, uint32_t bs = 256) {
-                hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+                if (bs != 1024)  // (the 1024-thread kernels' table is static LDS)
+                    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
                 const uint64_t gb = bs == 256 ? g : std::min<uint64_t>((n + bs - 1) / bs, probe_wgs_per_cu(2) * num_cus);
-                kern<<<dim3((uint32_t)std::max<uint64_t>(gb, 1)), dim3(bs), smem, st>>>(src, n, df, nfilt, rg,
-                                                                                           shared_k, md, out);
+                kern<<<dim3((uint32_t)std::max<uint64_t>(gb, 1)), dim3(bs), bs == 1024 ? 0 : smem, st>>>(
+                    src, n, df, nfilt, rg, shared_k, md, out);
             };
             if (tsz == 1) {
                 if (shared_k == 7 && std::is_same<Src, Fixed16>::value && Mod14::fits(shared_nb))
@@ -585,12 +598,13 @@ hipError_t probe_with(const Src& src, uint64_t n, const ProbeFilter* hf, uint32_
         const size_t ent = (size_t)(((uint64_t)nb + 31) / 32) * 32;  // 64-bit: nb + 31 wraps at 2^32-1
         const size_t tsz = nfilt <= 8 ? 1 : nfilt <= 16 ? 2 : 4;
         const size_t smem = ent * tsz;
-        if (smem <= 64 * 1024) {
+        if (smem <= kProbeTableBytes) {
             auto go = [&](auto kern, auto md, uint32_t bs = 256) {
-                hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+                if (bs != 1024)  // (the 1024-thread kernels' table is static LDS)
+                    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
                 const uint64_t gb = bs == 256 ? g : std::min<uint64_t>((n + bs - 1) / bs, probe_wgs_per_cu(1) * num_cus);
-                kern<<<dim3((uint32_t)std::max<uint64_t>(gb, 1)), dim3(bs), smem, st>>>(src, n, md, hf[0].k, nb,
-                                                                                           df, nfilt, stride, out);
+                kern<<<dim3((uint32_t)std::max<uint64_t>(gb, 1)), dim3(bs), bs == 1024 ? 0 : smem, st>>>(
+                    src, n, md, hf[0].k, nb, df, nfilt, stride, out);
             };
             const Mod32 m32 = hf[0].md;
             const bool w32 = fits_walk32(nb), k7 = hf[0].k == 7;

@@ -265,3 +265,21 @@ def test_walk_records_replay_the_walks(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout + out.stderr
+
+
+def test_reductions_at_quotient_edges(tmp_path):
+    """Mod32::reduce, Mod32::reduce31 (Walk32's 32-bit remainder path) and
+    Mod14::reduce against a literal 64-bit % at the inputs that stress their
+    biased-low quotient estimates: x = q*d + {0, 1, d-1} for extreme q, x near
+    0 and 2^64, multiples of d, over fixed edge moduli (2^30, 2^31, 2^32-1 ...)
+    and random ones (tests/cpp/reduce_test.cpp, host build of the device
+    header)."""
+    import subprocess
+    exe = str(tmp_path / "reduce_test")
+    src = os.path.join(ROOT, "tests", "cpp", "reduce_test.cpp")
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "--offload-arch=gfx950", src, "-o", exe],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert ", 0 bad" in out.stdout
