@@ -413,13 +413,17 @@ def main():
     ctx.set_timing(False)
     strategy = lsmbloom.build_strategy(nb, npg, k)
     alg_bytes = 16 * npg + 8 * nw
-    achieved = alg_bytes / (kt[0] * 1e-3) / 1e9
-    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-            "kernel": "build (%s: k_bin + k_apply)" % strategy,
-            "algorithmic_bytes": alg_bytes, "algorithmic_bytes_per_key": round(alg_bytes / npg, 3),
-            "kernel_ms": round(float(kt[0]), 4), "pass_a_ms": round(float(kt[1]), 4),
-            "pass_b_ms": round(float(kt[2]), 4)}
+    # C2 at N = 1; a C5 shard (125 M keys into 2^32-1 bits) at N = 8
+    main_leg = {(100_000_000, 956715292): "c2", (125_000_000, 4294967295): "c5"}.get((npg, nb))
+    roof = leg_roofline(main_leg, alg_bytes, kt[0], "build (%s: k_bin + k_apply + k_ovf_apply)" % strategy)
+    roof.update({"algorithmic_bytes_per_key": round(alg_bytes / npg, 3), "pass_a_ms": round(float(kt[1]), 4),
+                 "pass_b_ms": round(float(kt[2]), 4)})
+    if world == 1 and npg == 100_000_000:
+        roof["hash_walk_floor"] = {
+            "ms": HASH_WALK_FLOOR_MS_PER_1E8, "frac_of_hbm_roofline_at_that_time": round(
+                alg_bytes / (HASH_WALK_FLOOR_MS_PER_1E8 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "what": "XXH3-128 + 7 exact positions of 100 M 16-B keys alone, full occupancy (tools/mb_hash.hip): "
+                    "no build can beat this compute floor"}
 
     out = {"metric": "bloom build + batched probe, Mkeys/s device-resident, at 1/2/4/8 MI355X",
            "value": round(value, 2), "unit": "Mkeys/s", "n_gpus": world, "steps": args.steps,
@@ -513,15 +517,6 @@ def main():
     torch.cuda.empty_cache()
     if not args.no_varlen and world == 1:
         out["varlen"] = bench_varlen(ctx, dev, args)
-    tr = committed_traffic()
-    if tr and world == 1 and total == 100_000_000 and not args.filter_keys:
-        out["roofline"]["traffic_source"] = tr["source"]
-        if tr["fresh"]:
-            out["roofline"]["traffic"] = tr["bytes"]
-            if tr.get("valu_insts"):
-                out["roofline"]["secondary"] = valu_roofline(tr, out["roofline"]["kernel_ms"], npg, nb)
-        else:
-            out["roofline"]["traffic_stale"] = "kernel sources changed since %s was profiled" % tr["source"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(nb, k, args.cpu_seconds)
         out["cpu_baseline"]["gpu_over_cpu_1thread"] = round(value / out["cpu_baseline"]["value"], 1)
@@ -615,7 +610,9 @@ def bench_exact10(ctx, keys, n, reps=10):
            "value": round(n / (kt[0] * 1e-3) / 1e6, 1), "unit": "Mkeys/s", "kernel_ms": round(float(kt[0]), 4),
            "pass_a_ms": round(float(kt[1]), 4), "pass_b_ms": round(float(kt[2]), 4),
            "strategy": lsmbloom.build_strategy(nb, n, k),
-           "frac": round(alg / (kt[0] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+           "frac": round(alg / (kt[0] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "roofline": leg_roofline("exact10" if n == 100_000_000 else None, alg, kt[0],
+                                    "build (k_bin + k_apply + k_ovf_apply)")}
     # expected fill of an ideal filter: 1 - exp(-k n / m)
     res["fill_ratio"] = round(fill / nb, 5)
     res["fill_ratio_expected"] = round(1 - float(np.exp(-k * n / nb)), 5)
@@ -771,7 +768,9 @@ def bench_varlen(ctx, dev, args):
            "pass_b_ms": round(float(kt[2]), 4), "algorithmic_bytes": alg,
            "achieved_GBs": round(alg / (kt[0] * 1e-3) / 1e9, 1),
            "frac": round(alg / (kt[0] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-           "strategy": lsmbloom.build_strategy(nb, n)}
+           "strategy": lsmbloom.build_strategy(nb, n),
+           "roofline": leg_roofline("c4" if n == 100_000_000 else None, alg, kt[0],
+                                    "build (k_hash_var + k_bin<Recs> + k_apply + k_ovf_apply)")}
     if n == 100_000_000:
         res["words_equal_oracle_fixture"] = fixture_check(words, "c4", nb)
     del data, offs, words
@@ -779,60 +778,94 @@ def bench_varlen(ctx, dev, args):
     return res
 
 
-BUILD_SOURCES = ("storage-engine_amd/csrc/bloom_build.hip", "storage-engine_amd/csrc/kernels.hpp",
-                 "storage-engine_amd/csrc/bloom_math.hpp", "storage-engine_amd/csrc/xxh3.hpp",
-                 "storage-engine_amd/csrc/keysrc.hpp")
+KERNEL_SOURCES = ("storage-engine_amd/csrc/bloom_build.hip", "storage-engine_amd/csrc/bloom_probe.hip",
+                  "storage-engine_amd/csrc/kernels.hpp", "storage-engine_amd/csrc/bloom_math.hpp",
+                  "storage-engine_amd/csrc/xxh3.hpp", "storage-engine_amd/csrc/keysrc.hpp",
+                  "storage-engine_amd/csrc/hash_var.hpp")
 
 
 def build_sources_sha():
-    """sha256 over the C2 build kernels' sources: stamps profiles/traffic.json."""
+    """sha256 over the build and probe kernels' sources: stamps profiles/traffic.json."""
     import hashlib
     h = hashlib.sha256()
-    for p in BUILD_SOURCES:
+    for p in KERNEL_SOURCES:
         with open(os.path.join(ROOT, p), "rb") as f:
             h.update(f.read())
     return h.hexdigest()[:16]
 
 
-def committed_traffic():
-    """HBM bytes per C2 build from the committed rocprofv3 PMC summary
-    (profiles/traffic.json, written by tools/prof_summary.py --json from separate
-    FETCH_SIZE / WRITE_SIZE passes of this bench; FETCH_SIZE doubled per the
-    gfx950 note in MI355X_MICROARCH.md).  `fresh` is False when the build
-    kernels' sources changed since that profile (its stamped sha differs)."""
+def committed_legs():
+    """Per-leg PMC figures from the committed rocprofv3 summary
+    (profiles/traffic.json, tools/profile_legs.sh + tools/prof_summary.py
+    --legs: every leg in a process of its own, separate FETCH_SIZE /
+    WRITE_SIZE / SQ passes, FETCH_SIZE doubled per the gfx950 note in
+    MI355X_MICROARCH.md).  `fresh` is False when the kernels' sources changed
+    since that profile (its stamped sha differs)."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(p):
         return None
     t = json.load(open(p))
-    return {"bytes": t.get("build_bytes"), "source": "%s (%s)" % (os.path.relpath(p, ROOT), t.get("profile")),
-            "fresh": t.get("kernel_src_sha") == build_sources_sha(), "valu_insts": t.get("build_valu_insts")}
+    if t.get("format") != 2:
+        return None
+    return {"legs": t["legs"], "source": "%s (%s)" % (os.path.relpath(p, ROOT), t.get("profile")),
+            "fresh": t.get("kernel_src_sha") == build_sources_sha()}
 
 
-# VALU issue ceiling: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2
-# cycles per SIMD (SIMD-32), 2.4 GHz (MI355X_MICROARCH.md: execution model).
-VALU_PEAK_WAVE_INSTS = 256 * 4 * 2.4e9 / 2
-# XXH3-128 of 16-B keys + the 7 exact positions alone (no binning, no filter
-# traffic), 100 M keys at full occupancy: tools/mb_hash.hip (DESIGN.md 4.1).
-HASH_WALK_FLOOR_MS_PER_1E8 = 0.47
+# Ceilings of the secondary units, per profiled launch (clock-independent: the
+# launch's own cycles from GRBM_GUI_ACTIVE, summed over the 8 XCDs).
+# VALU: a wave64 instruction occupies its SIMD ~4 cycles (tools/mb_valu.hip,
+# profiles/r04/r04b_valu_issue.jsonl: 4.1-4.7 for the multiplies, converts,
+# f64, min, bfe and 64-bit ops; 2.3-2.5 for add / xor / mul_f32), 1024 SIMDs.
+# LDS: SQ_LDS_IDX_ACTIVE = LDS-array cycles over the 256 CUs' LDS.
+VALU_CYCLES_PER_INST = 4.0
+HASH_WALK_FLOOR_MS_PER_1E8 = 0.47  # XXH3-128 of 16-B keys + 7 exact positions, full occupancy (tools/mb_hash.hip)
 
 
-def valu_roofline(tr, kernel_ms, n, num_bits):
-    """roofline.secondary: the build's VALU work against the VALU issue
-    ceiling, from the committed PMC profile's SQ_INSTS_VALU (whole-chip wave64
-    VALU instructions per build).  Quarter-rate instructions (the 64-bit
-    multiplies of XXH3 and of the exact reductions) take longer than the 2
-    cycles counted here, so the true ceiling is lower: frac is a lower bound
-    on how busy the VALU is."""
-    insts = tr["valu_insts"]
-    achieved = insts / (kernel_ms * 1e-3)
-    return {"bound": "valu", "achieved": round(achieved / 1e12, 4), "peak": round(VALU_PEAK_WAVE_INSTS / 1e12, 4),
-            "unit": "T wave64-VALU-inst/s", "frac": round(achieved / VALU_PEAK_WAVE_INSTS, 4),
-            "valu_insts_per_build": insts, "valu_insts_per_wave_key": round(insts * 64 / n, 1),
-            "valu_issue_floor_ms": round(insts / VALU_PEAK_WAVE_INSTS * 1e3, 4),
-            "hash_walk_floor_ms": round(HASH_WALK_FLOOR_MS_PER_1E8 * n / 1e8, 4),
-            "hash_walk_floor_frac_of_hbm_roofline": round(
-                (16 * n + 8 * ((num_bits + 63) // 64)) / (HASH_WALK_FLOOR_MS_PER_1E8 * n / 1e8 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "source": tr["source"]}
+def leg_roofline(leg, alg_bytes, kernel_ms, kernel, legs=None):
+    """roofline object of one bench leg: algorithmic HBM bytes per launch over
+    the launch's kernel time (HIP events) against 8 TB/s; `traffic` = HBM
+    bytes per launch from the committed PMC passes; `secondary` = how busy the
+    VALU and the LDS were in the profiled launch, and `limiter` = the busiest
+    of HBM (measured traffic), VALU and LDS."""
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kernel,
+            "algorithmic_bytes": int(alg_bytes), "kernel_ms": round(float(kernel_ms), 4)}
+    legs = legs if legs is not None else committed_legs()
+    if not legs or leg not in legs["legs"]:
+        return roof
+    roof["traffic_source"] = legs["source"]
+    if not legs["fresh"]:
+        roof["traffic_stale"] = "kernel sources changed since %s was profiled" % legs["source"]
+        return roof
+    p = legs["legs"][leg]["per_launch"]
+    roof["traffic"] = p.get("hbm_bytes")
+    cyc = p.get("grbm_gui_active", 0) / 8.0
+    prof_us = p.get("kernel_us")
+    sec = {}
+    if prof_us:
+        sec["hbm_measured"] = {"achieved": round(p["hbm_bytes"] / (prof_us * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                               "unit": "GB/s", "frac": round(p["hbm_bytes"] / (prof_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                               "what": "PMC traffic over the profiled launch's kernel time"}
+    if cyc > 0 and p.get("valu_insts"):
+        sec["valu"] = {"insts_per_launch": p["valu_insts"], "cycles_per_inst": VALU_CYCLES_PER_INST,
+                       "frac": round(p["valu_insts"] * VALU_CYCLES_PER_INST / (1024 * cyc), 4),
+                       "what": "wave64 VALU instructions x 4 cycles / (1024 SIMDs x the launch's cycles)"}
+    if cyc > 0 and p.get("lds_idx_active") is not None:
+        la = p["lds_idx_active"]
+        sec["lds"] = {"array_cycles_per_launch": la, "frac": round(la / (256 * cyc), 4),
+                      "bank_conflict_share": round(p.get("lds_bank_conflict", 0) / la, 4) if la else None,
+                      "insts_per_launch": p.get("lds_insts"),
+                      "issue_est_frac": round(p.get("lds_insts", 0) * 10.1 / (256 * cyc), 4),
+                      "what": "SQ_LDS_IDX_ACTIVE (LDS-array cycles) / (256 CUs x the launch's cycles); "
+                              "issue_est: SQ_INSTS_LDS x 10.1 cycles (ds_add_rtn, tools/mb_lds.hip)"}
+    if sec:
+        sec["launch_cycles"] = int(cyc)
+        roof["secondary"] = sec
+        cand = {k: v["frac"] for k, v in sec.items() if isinstance(v, dict) and "frac" in v}
+        if cand:
+            roof["limiter"] = max(cand, key=cand.get)
+    return roof
 
 
 def fixture_check(words, name, num_bits):
@@ -854,115 +887,148 @@ def fixture_check(words, name, num_bits):
                 and hashlib.sha256(w.tobytes()).hexdigest() == fx["sha256"])
 
 
+class ProbeLegs:
+    """C3's data (configs[2]) and its three device probes, shared by
+    bench_probe and tools/legs.py (rocprofv3 passes per leg): F per-SSTable
+    filters sized like SSTableBuilder::new (1000 keys, 0.01) and Q lookup keys
+    (50 % members drawn across the F filters, 50 % fresh).
+      probe()       lsmb_probe_dev over the F filters (k_probe_sliced)
+      fset()        lsmb_fset_probe_dev, the same F tables with their key ranges
+      fset_mixed()  a set of two sizes: F/2 of them + F/2 x new(4000, 0.01)"""
+
+    def __init__(self, ctx, dev, Q, F):
+        import numpy as np
+        import torch
+
+        import lsmbloom
+        self.ctx, self.dev, self.Q, self.F = ctx, dev, Q, F
+        nb, k = lsmbloom.params(1000, 0.01)
+        self.nb, self.k = nb, k
+        nw = lsmbloom.num_words(nb)
+        self.filt = []
+        self.members = torch.empty((F * 1000, 16), dtype=torch.uint8, device=dev)
+        for f in range(F):
+            ctx.gen_key16_dev(0xF000 + f, 0, 1000, self.members[f * 1000:(f + 1) * 1000])
+            w = torch.zeros(nw, dtype=torch.int64, device=dev)
+            ctx.build_fixed_dev(self.members[f * 1000:(f + 1) * 1000], 16, 1000, nb, k, w)
+            self.filt.append((w, nb, k))
+        self.q = torch.empty((Q, 16), dtype=torch.uint8, device=dev)
+        ctx.gen_key16_dev(SEED_FRESH, 0, Q, self.q)
+        g = torch.Generator(device="cpu").manual_seed(1)
+        self.sel = torch.randint(0, F * 1000, (Q // 2,), generator=g).to(dev)
+        self.q[: Q // 2] = self.members[self.sel]
+        self.out = torch.zeros((Q, (F + 7) // 8), dtype=torch.uint8, device=dev)
+        self.fout = torch.zeros(Q, dtype=torch.int64, device=dev)
+        # the same F tables as a filter set, with their key ranges
+        self.fs = lsmbloom.FilterSet(ctx)
+        self.slots = []
+        for f in range(F):
+            rows = self.members[f * 1000:(f + 1) * 1000].cpu().numpy()
+            srt = sorted(bytes(r) for r in rows)
+            self.slots.append(self.fs.add_filter(
+                lsmbloom.BloomFilter(self.filt[f][0].cpu().numpy().view(np.uint64), k, nb), srt[0], srt[-1]))
+        # mixed sizes: F/2 of the C3 tables + F/2 compaction-sized new(4000, 0.01)
+        # (38 271 bits): two (num_bits, k) classes, each its own LDS table
+        self.fsm = lsmbloom.FilterSet(ctx)
+        nb4, k4 = lsmbloom.params(4000, 0.01)
+        big = torch.empty((4000, 16), dtype=torch.uint8, device=dev)
+        for f in range(F):
+            if f < F // 2:
+                rows = self.members[f * 1000:(f + 1) * 1000].cpu().numpy()
+                bf = lsmbloom.BloomFilter(self.filt[f][0].cpu().numpy().view(np.uint64), k, nb)
+            else:
+                ctx.gen_key16_dev(0xF100 + f, 0, 4000, big)
+                w4 = torch.zeros(lsmbloom.num_words(nb4), dtype=torch.int64, device=dev)
+                ctx.build_fixed_dev(big, 16, 4000, nb4, k4, w4)
+                rows = big.cpu().numpy()
+                bf = lsmbloom.BloomFilter(w4.cpu().numpy().view(np.uint64), k4, nb4)
+            srt = sorted(bytes(r) for r in rows)
+            self.fsm.add_filter(bf, srt[0], srt[-1])
+        self.nw = nw
+
+    def probe(self):
+        self.ctx.probe_dev(self.filt, self.q, self.Q, self.out, key_len=16)
+
+    def fset(self):
+        self.fs.probe_dev(self.q, self.Q, self.fout, key_len=16)
+
+    def fset_mixed(self):
+        self.fsm.probe_dev(self.q, self.Q, self.fout, key_len=16)
+
+    def alg_bytes(self, leg):
+        """Algorithmic HBM bytes of one launch: the keys, the answers and the filters."""
+        if leg == "probe":
+            return self.Q * 16 + self.Q * self.out.shape[1] + self.F * (12 + 8 * self.nw)
+        return self.Q * 16 + self.Q * 8 + self.F * (12 + 8 * self.nw)
+
+    def close(self):
+        self.fs.close()
+        self.fsm.close()
+
+
+def timed_ms(fn, warmup, steps):
+    """Average ms of fn() over `steps` calls (HIP events on the current stream)."""
+    import torch
+    for _ in range(max(1, warmup)):
+        fn()
+    torch.cuda.synchronize()
+    st = torch.cuda.Event(enable_timing=True)
+    en = torch.cuda.Event(enable_timing=True)
+    st.record()
+    for _ in range(steps):
+        fn()
+    en.record()
+    torch.cuda.synchronize()
+    return st.elapsed_time(en) / steps
+
+
 def bench_probe(ctx, dev, args, world=1, rank=0, max_over_ranks=lambda x: x):
     """C3: Q lookup keys (50% members drawn across the F filters, 50% fresh)
     against F per-SSTable filters sized like SSTableBuilder::new (1000 keys, 0.01).
     N > 1: the filters are replicated and the queries partitioned (no
     collective); the rate counts all ranks' queries over the slowest rank."""
-    import numpy as np
     import torch
 
-    import lsmbloom
     F, Q_all = args.probe_filters, args.probe_keys
     Q = Q_all // world
-    nb, k = lsmbloom.params(1000, 0.01)
-    nw = lsmbloom.num_words(nb)
-    filt = []
-    members = torch.empty((F * 1000, 16), dtype=torch.uint8, device=dev)
-    for f in range(F):
-        ctx.gen_key16_dev(0xF000 + f, 0, 1000, members[f * 1000:(f + 1) * 1000])
-        w = torch.zeros(nw, dtype=torch.int64, device=dev)
-        ctx.build_fixed_dev(members[f * 1000:(f + 1) * 1000], 16, 1000, nb, k, w)
-        filt.append((w, nb, k))
-    q = torch.empty((Q, 16), dtype=torch.uint8, device=dev)
-    ctx.gen_key16_dev(SEED_FRESH, 0, Q, q)
-    g = torch.Generator(device="cpu").manual_seed(1)
-    sel = torch.randint(0, F * 1000, (Q // 2,), generator=g).to(dev)
-    q[: Q // 2] = members[sel]
-    out = torch.zeros((Q, (F + 7) // 8), dtype=torch.uint8, device=dev)
-    for _ in range(max(1, args.warmup)):
-        ctx.probe_dev(filt, q, Q, out, key_len=16)
-    torch.cuda.synchronize(dev)
-    st = torch.cuda.Event(enable_timing=True)
-    en = torch.cuda.Event(enable_timing=True)
-    st.record()
-    for _ in range(args.steps):
-        ctx.probe_dev(filt, q, Q, out, key_len=16)
-    en.record()
-    torch.cuda.synchronize(dev)
-    ms = max_over_ranks(st.elapsed_time(en) / args.steps)
-    alg = Q * 16 + Q * out.shape[1] + F * (12 + 8 * nw)
-    hits = int((out[: Q // 2] != 0).all(dim=1).sum().item())
+    P = ProbeLegs(ctx, dev, Q, F)
+    ms = max_over_ranks(timed_ms(P.probe, args.warmup, args.steps))
+    alg = P.alg_bytes("probe")
+    hits = int((P.out[: Q // 2] != 0).all(dim=1).sum().item())
     res = {"workload": "C3 (configs[2]): %d 16-B keys x %d filters new(1000, 0.01) (%d bits, k=%d)%s"
-                       % (Q_all, F, nb, k, ", %d per GPU" % Q if world > 1 else ""),
+                       % (Q_all, F, P.nb, P.k, ", %d per GPU" % Q if world > 1 else ""),
            "value": round(Q * world / (ms * 1e-3) / 1e6, 2), "unit": "Mkeys/s", "ms": round(ms, 4),
-           "achieved_GBs": round(alg / (ms * 1e-3) / 1e9, 1), "member_rows_all_hit": hits == Q // 2}
+           "achieved_GBs": round(alg / (ms * 1e-3) / 1e9, 1), "algorithmic_bytes": alg,
+           "member_rows_all_hit": hits == Q // 2,
+           "roofline": leg_roofline("probe" if (Q, F) == (10_000_000, 8) else None, alg, ms, "k_probe_sliced")}
     # Every answer of the full-size run against the oracle's (digests committed
     # in tests/golden/c3_fixture.json by gen_c3_fixture.py; outside the timing).
     c3fx = c3_fixture() if world == 1 else None
     if c3fx and c3fx["Q"] == Q and c3fx["F"] == F:
-        res["answers_equal_oracle_fixture"] = _sha(out) == c3fx["probe_mask_sha256"]
+        res["answers_equal_oracle_fixture"] = _sha(P.out) == c3fx["probe_mask_sha256"]
     # The same batch through the device-resident filter set (lsmb_fset): per
     # key and SSTable, min_key <= key <= max_key && may_contain — the checks
     # SSTable::get makes (src/sstable/reader.rs:192-199) — for all 8 tables.
-    fs = lsmbloom.FilterSet(ctx)
-    slots = []
-    for f in range(F):
-        rows = members[f * 1000:(f + 1) * 1000].cpu().numpy()
-        srt = sorted(bytes(r) for r in rows)
-        slots.append(fs.add_filter(lsmbloom.BloomFilter(filt[f][0].cpu().numpy().view(np.uint64), k, nb),
-                                   srt[0], srt[-1]))
-    fout = torch.zeros(Q, dtype=torch.int64, device=dev)
-    for _ in range(max(1, args.warmup)):
-        fs.probe_dev(q, Q, fout, key_len=16)
-    torch.cuda.synchronize(dev)
-    st.record()
-    for _ in range(args.steps):
-        fs.probe_dev(q, Q, fout, key_len=16)
-    en.record()
-    torch.cuda.synchronize(dev)
-    fms = max_over_ranks(st.elapsed_time(en) / args.steps)
+    fms = max_over_ranks(timed_ms(P.fset, args.warmup, args.steps))
     # a member row's own table must answer 1 (range and bloom); here sel // 1000
-    own = (fout[: Q // 2] >> torch.tensor(slots, device=dev)[sel // 1000]) & 1
+    own = (P.fout[: Q // 2] >> torch.tensor(P.slots, device=dev)[P.sel // 1000]) & 1
     res["fset"] = {"what": "lsmb_fset_probe_dev: range pre-check + bloom, %d tables, u64 mask per key" % F,
                    "value": round(Q * world / (fms * 1e-3) / 1e6, 2), "unit": "Mkeys/s", "ms": round(fms, 4),
-                   "member_rows_own_table_hit": bool(own.all().item())}
+                   "algorithmic_bytes": P.alg_bytes("fset"), "member_rows_own_table_hit": bool(own.all().item()),
+                   "roofline": leg_roofline("fset" if (Q, F) == (10_000_000, 8) else None, P.alg_bytes("fset"), fms,
+                                            "k_fset_sliced")}
     if c3fx and c3fx["Q"] == Q and c3fx["F"] == F:
-        res["fset"]["answers_equal_oracle_fixture"] = _sha(fout) == c3fx["fset_mask_sha256"]
-    fs.close()
-    # Mixed sizes: 4 of the C3 tables next to 4 compaction-sized ones
-    # (new(4000, 0.01), 38 271 bits): two (num_bits, k) classes, each its own
-    # bit-sliced LDS table (k_fset_classes).
-    fs = lsmbloom.FilterSet(ctx)
-    nb4, k4 = lsmbloom.params(4000, 0.01)
-    big = torch.empty((4000, 16), dtype=torch.uint8, device=dev)
-    for f in range(F):
-        if f < F // 2:
-            rows = members[f * 1000:(f + 1) * 1000].cpu().numpy()
-            bf = lsmbloom.BloomFilter(filt[f][0].cpu().numpy().view(np.uint64), k, nb)
-        else:
-            ctx.gen_key16_dev(0xF100 + f, 0, 4000, big)
-            w4 = torch.zeros(lsmbloom.num_words(nb4), dtype=torch.int64, device=dev)
-            ctx.build_fixed_dev(big, 16, 4000, nb4, k4, w4)
-            rows = big.cpu().numpy()
-            bf = lsmbloom.BloomFilter(w4.cpu().numpy().view(np.uint64), k4, nb4)
-        srt = sorted(bytes(r) for r in rows)
-        fs.add_filter(bf, srt[0], srt[-1])
-    for _ in range(max(1, args.warmup)):
-        fs.probe_dev(q, Q, fout, key_len=16)
-    torch.cuda.synchronize(dev)
-    st.record()
-    for _ in range(args.steps):
-        fs.probe_dev(q, Q, fout, key_len=16)
-    en.record()
-    torch.cuda.synchronize(dev)
-    mms = max_over_ranks(st.elapsed_time(en) / args.steps)
+        res["fset"]["answers_equal_oracle_fixture"] = _sha(P.fout) == c3fx["fset_mask_sha256"]
+    mms = max_over_ranks(timed_ms(P.fset_mixed, args.warmup, args.steps))
     res["fset_mixed"] = {"what": "lsmb_fset_probe_dev, %d tables of two sizes: %d x new(1000, 0.01) + %d x "
                                  "new(4000, 0.01), one LDS table per size class" % (F, F // 2, F - F // 2),
-                         "value": round(Q * world / (mms * 1e-3) / 1e6, 2), "unit": "Mkeys/s", "ms": round(mms, 4)}
+                         "value": round(Q * world / (mms * 1e-3) / 1e6, 2), "unit": "Mkeys/s", "ms": round(mms, 4),
+                         "algorithmic_bytes": P.alg_bytes("fset_mixed"),
+                         "roofline": leg_roofline("fset_mixed" if (Q, F) == (10_000_000, 8) else None,
+                                                  P.alg_bytes("fset_mixed"), mms, "k_fset_classes")}
     if c3fx and c3fx["Q"] == Q and c3fx["F"] == F:
-        res["fset_mixed"]["answers_equal_oracle_fixture"] = _sha(fout) == c3fx["fset_mixed_mask_sha256"]
-    fs.close()
+        res["fset_mixed"]["answers_equal_oracle_fixture"] = _sha(P.fout) == c3fx["fset_mixed_mask_sha256"]
+    P.close()
     return res
 
 

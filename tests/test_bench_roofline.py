@@ -1,0 +1,39 @@
+"""bench.py's per-leg roofline objects from a per-leg
+PMC summary (profiles/traffic.json format 2): HBM frac from the algorithmic
+bytes, traffic from the PMC passes, VALU / LDS busy fractions over the
+launch's own cycles, and the stale guard when the kernels' sources change."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def _legs(fresh=True):
+    return {"source": "profiles/traffic.json (test)", "fresh": fresh, "legs": {"c2": {"per_launch": {
+        "hbm_bytes": 6_000_000_000, "read_bytes": 3_500_000_000, "write_bytes": 2_500_000_000,
+        "kernel_us": 1500.0, "valu_insts": 400_000_000, "lds_insts": 50_000_000,
+        "lds_idx_active": 200_000_000, "lds_bank_conflict": 120_000_000, "grbm_gui_active": 8 * 3_000_000}}}}
+
+
+def test_leg_roofline_fractions():
+    r = bench.leg_roofline("c2", 1_719_589_416, 1.4, "build", legs=_legs())
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert abs(r["frac"] - 1_719_589_416 / 1.4e-3 / 1e9 / 8000) < 1e-4
+    assert r["traffic"] == 6_000_000_000
+    sec = r["secondary"]
+    assert sec["launch_cycles"] == 3_000_000
+    assert abs(sec["valu"]["frac"] - 400e6 * 4 / (1024 * 3e6)) < 1e-4
+    assert abs(sec["lds"]["frac"] - 200e6 / (256 * 3e6)) < 1e-4
+    assert abs(sec["lds"]["bank_conflict_share"] - 0.6) < 1e-4
+    assert abs(sec["hbm_measured"]["frac"] - 6e9 / 1.5e-3 / 1e9 / 8000) < 1e-4
+    assert r["limiter"] == max(("hbm_measured", "valu", "lds"), key=lambda k: sec[k]["frac"])
+
+
+def test_leg_roofline_stale_and_missing():
+    r = bench.leg_roofline("c2", 1e9, 1.0, "build", legs=_legs(fresh=False))
+    assert r["traffic"] is None and "traffic_stale" in r and "secondary" not in r
+    r = bench.leg_roofline("probe", 1e8, 0.05, "k_probe_sliced", legs=_legs())
+    assert r["traffic"] is None and "secondary" not in r and abs(r["frac"] - 1e8 / 0.05e-3 / 1e9 / 8000) < 1e-4

@@ -108,8 +108,96 @@ def pmc(d, subs, title):
         print()
 
 
+# per-leg profiles (tools/profile_legs.sh: one process per bench leg, 10 launches)
+LEG_KERNELS = {
+    "c2": ("k_bin", "k_apply", "k_ovf_apply"),
+    "exact10": ("k_bin", "k_apply", "k_ovf_apply"),
+    "c5": ("k_bin", "k_apply", "k_ovf_apply"),
+    "c4": ("k_hash_var", "k_bin", "k_apply", "k_ovf_apply"),
+    "probe": ("k_probe_sliced",),
+    "fset": ("k_fset_sliced",),
+    "fset_mixed": ("k_fset_classes",),
+}
+LEG_REPS = 10
+COUNTERS = {"FETCH_SIZE": "read_bytes", "WRITE_SIZE": "write_bytes", "SQ_INSTS_VALU": "valu_insts",
+            "SQ_INSTS_LDS": "lds_insts", "SQ_LDS_IDX_ACTIVE": "lds_idx_active",
+            "SQ_LDS_BANK_CONFLICT": "lds_bank_conflict", "SQ_WAVE_CYCLES": "wave_cycles",
+            "SQ_BUSY_CYCLES": "busy_cycles", "SQ_WAIT_ANY": "wait_any", "SQ_INSTS_SALU": "salu_insts",
+            "GRBM_GUI_ACTIVE": "grbm_gui_active"}
+
+
+def leg_data(d, leg):
+    """Per kernel of the leg: launches per leg iteration, mean duration and
+    the mean of every counter per dispatch; and their per-iteration sums."""
+    pre = LEG_KERNELS[leg]
+    kern = collections.defaultdict(dict)
+    ks = os.path.join(d, leg, "stats", "run_kernel_stats.csv")
+    if os.path.exists(ks):
+        for r in csv.DictReader(open(ks)):
+            kn = short(r["Name"])
+            if kn.startswith(pre):
+                kern[kn]["calls_per_launch"] = round(int(r["Calls"]) / LEG_REPS, 3)
+                kern[kn]["avg_us"] = round(float(r["AverageNs"]) / 1e3, 3)
+    for sub in ("fetch", "write", "sq"):
+        p = os.path.join(d, leg, sub, "run_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        vals = collections.defaultdict(lambda: collections.defaultdict(list))
+        for r in csv.DictReader(open(p)):
+            kn = short(r["Kernel_Name"])
+            if kn.startswith(pre) and r["Counter_Name"] in COUNTERS:
+                vals[kn][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for kn, cv in vals.items():
+            for cn, v in cv.items():
+                m = sum(v) / len(v)
+                if cn == "FETCH_SIZE":
+                    m = 2 * m * 1024  # KiB, x2 on gfx950 (MI355X_MICROARCH.md, HBM section)
+                elif cn == "WRITE_SIZE":
+                    m = m * 1024
+                kern[kn][COUNTERS[cn]] = int(m)
+    per = collections.Counter()
+    for kn, m in kern.items():
+        c = m.get("calls_per_launch", 1.0)
+        for key in list(COUNTERS.values()) + ["avg_us"]:
+            if key in m:
+                per[key] += m[key] * c
+    out = {k: (round(v, 3) if k == "avg_us" else int(v)) for k, v in per.items()}
+    if "avg_us" in out:
+        out["kernel_us"] = out.pop("avg_us")
+    out["hbm_bytes"] = out.get("read_bytes", 0) + out.get("write_bytes", 0)
+    return {"kernels": dict(kern), "per_launch": out}
+
+
+def legs_json(d, out):
+    import json
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    legs = {leg: leg_data(d, leg) for leg in LEG_KERNELS if os.path.isdir(os.path.join(d, leg))}
+    json.dump({"profile": os.path.basename(d.rstrip("/")), "format": 2, "kernel_src_sha": bench.build_sources_sha(),
+               "legs": legs,
+               "note": "per leg iteration (one build / one probe call): sums over its kernels of the mean per "
+                       "dispatch x dispatches per iteration; FETCH_SIZE x2 (gfx950), KiB -> B; separate --pmc passes"},
+              open(out, "w"), indent=1)
+    print("# per-leg rocprofv3 summary: %s\n" % os.path.basename(d.rstrip("/")))
+    print("| leg | kernel us | HBM read MB | HBM write MB | VALU inst | LDS inst | LDS-array cycles | GRBM_GUI_ACTIVE |")
+    print("|---|---|---|---|---|---|---|---|")
+    for leg, v in legs.items():
+        p = v["per_launch"]
+        print("| %s | %s | %.1f | %.1f | %.4g | %.4g | %.4g | %.4g |" % (
+            leg, p.get("kernel_us"), p.get("read_bytes", 0) / 1e6, p.get("write_bytes", 0) / 1e6,
+            p.get("valu_insts", 0), p.get("lds_insts", 0), p.get("lds_idx_active", 0), p.get("grbm_gui_active", 0)))
+    print()
+    for leg, v in legs.items():
+        print("## %s\n" % leg)
+        for kn, m in v["kernels"].items():
+            print("- **%s**: %s" % (kn, ", ".join("%s=%s" % (a, b) for a, b in sorted(m.items()))))
+        print()
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 3 and sys.argv[2] == "--json":
         traffic_json(sys.argv[1], sys.argv[3])
+    elif len(sys.argv) > 3 and sys.argv[2] == "--legs":
+        legs_json(sys.argv[1], sys.argv[3])
     else:
         main(sys.argv[1])
