@@ -49,6 +49,34 @@ __device__ __forceinline__ void store_row(uint8_t* out, uint64_t i, uint32_t str
     }
 }
 
+// Grid-wide rounds over n items for the 1024-thread C3 probe: round j is
+// items [j*gs, (j+1)*gs), lane L of the grid takes item j*gs + L.  Each
+// round's keys and rows are addressed through a buffer resource whose base
+// the scalar unit advances: no 64-bit lane addresses, indices or bounds
+// compares, and the last round's out-of-range lanes load zeros and their
+// stores are dropped by the resource's num_records (windows past the last
+// round are empty).  The counts are made scalar with readfirstlane, so every
+// window bound is SALU work; launchers keep n below 2^40 (rounds < 2^31).
+struct Rounds {
+    uint32_t gs, lane, rounds, last;
+    __device__ __forceinline__ Rounds(uint64_t n, uint32_t bs) {
+        gs = gridDim.x * bs;
+        lane = blockIdx.x * bs + threadIdx.x;
+        rounds = (uint32_t)__builtin_amdgcn_readfirstlane((int)((n + gs - 1) / gs));
+        last = (uint32_t)__builtin_amdgcn_readfirstlane((int)(n - (uint64_t)(rounds - 1) * gs));
+    }
+    // round j's window of `unit`-byte items at base
+    __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t j, uint32_t unit) const {
+        const uint32_t full = j + 1 < rounds ? gs : last;  // two scalar selects, no branches
+        const uint32_t cnt = j < rounds ? full : 0u;
+        return __builtin_amdgcn_make_buffer_rsrc((void*)((const uint8_t*)base + (uint64_t)j * (gs * unit)), 0,
+                                                 (int)(cnt * unit), 0x00020000);
+    }
+    __device__ __forceinline__ u32x4 keys16(const uint4* k, uint32_t j) const {
+        return __builtin_amdgcn_raw_buffer_load_b128(rsrc(k, j, 16), lane * 16, 0, 2 /* nt */);
+    }
+};
+
 // T holds up to 8*sizeof(T) filters' bits per position.
 // W: Walk32 when num_bits <= 2^31 (every intermediate fits 32 bits), else
 // Walk64.  K > 0: k fixed at compile time (7 = BloomFilter::new at fpr 0.01).
@@ -70,31 +98,58 @@ __global__ __launch_bounds__(BS) void k_probe_sliced(Src src, uint64_t n, typena
     __shared__ __align__(16) uint8_t smem_stat[BS == 1024 ? kProbeTableBytes : 16];
     uint8_t* const smem_raw = BS == 1024 ? smem_stat : smem_dyn;
     T* table = reinterpret_cast<T*>(smem_raw);
+    // The C3 instantiation (16-B keys, one-byte rows, k = 7, 1024 threads)
+    // walks the keys in Rounds; its first keys are requested before the
+    // table is built, so that load's latency overlaps the filter-word loads
+    // instead of following them.
+    constexpr bool kRounds = std::is_same<Src, Fixed16>::value && BS == 1024 && K > 0 && sizeof(T) == 1;
+    const Rounds R(kRounds ? n : 1, BS);
+    auto round_keys = [&](uint32_t j) -> u32x4 {
+        if constexpr (kRounds)
+            return R.keys16(src.k, j);
+        else
+            return u32x4{0, 0, 0, 0};
+    };
+    // Three rounds in flight: round j + 3 is requested once round j is done,
+    // so each load has two rounds of hashing (~4 K cycles at 4 waves per
+    // SIMD) to arrive.  The scheduling barriers keep the rounds in program
+    // order: left alone, the scheduler interleaves the three independent
+    // rounds and the loop head then waits for every load.
+    u32x4 ka = round_keys(0);
+    __builtin_amdgcn_sched_barrier(0);
+    u32x4 kb = round_keys(1);
+    __builtin_amdgcn_sched_barrier(0);
+    u32x4 kc = round_keys(2);
+    __builtin_amdgcn_sched_barrier(0);
     const uint32_t nw32 = (uint32_t)(((uint64_t)num_bits + 31) / 32);  // 64-bit: num_bits may be 2^32-1
     // The filters' word pointers and output bits, loaded once and all at
     // once (a per-filter descriptor -> word load chain would serialise 2F
     // global round trips before the first key).
+    // Branch-free: an absent filter slot re-reads filter 0's words under a
+    // zero mask.  (Per-slot branches here also cost the round loop below its
+    // load overlap: the compiler's wait analysis then made its head wait for
+    // every key load in flight.)
     constexpr uint32_t FMAX = 8 * sizeof(T);
     const uint32_t* wp[FMAX];
-    uint32_t ob[FMAX];
+    uint32_t ob[FMAX], vm[FMAX];
 #pragma unroll
     for (uint32_t f = 0; f < FMAX; f++) {
-        wp[f] = f < nfilt ? filters[f].words32 : nullptr;
-        ob[f] = f < nfilt ? filters[f].out_bit : 0;
+        const uint32_t g = f < nfilt ? f : 0u;
+        wp[f] = filters[g].words32;
+        ob[f] = filters[g].out_bit;
+        vm[f] = f < nfilt ? 1u : 0u;
     }
     for (uint32_t w = threadIdx.x; w < nw32; w += blockDim.x) {
         uint32_t xs[FMAX];
 #pragma unroll
-        for (uint32_t f = 0; f < FMAX; f++) xs[f] = f < nfilt ? wp[f][w] : 0u;
+        for (uint32_t f = 0; f < FMAX; f++) xs[f] = wp[f][w];
         T acc[32];
 #pragma unroll
         for (int b = 0; b < 32; b++) acc[b] = 0;
 #pragma unroll
         for (uint32_t f = 0; f < FMAX; f++) {
-            if (f < nfilt) {
 #pragma unroll
-                for (int b = 0; b < 32; b++) acc[b] |= (T)((T)((xs[f] >> b) & 1u) << ob[f]);
-            }
+            for (int b = 0; b < 32; b++) acc[b] |= (T)((T)((xs[f] >> b) & vm[f]) << ob[f]);
         }
 #pragma unroll
         for (int b = 0; b < 32; b++) table[w * 32 + b] = acc[b];
@@ -102,6 +157,33 @@ __global__ __launch_bounds__(BS) void k_probe_sliced(Src src, uint64_t n, typena
     __syncthreads();
     T all = 0;
     for (uint32_t f = 0; f < nfilt; f++) all |= (T)((T)1 << filters[f].out_bit);
+    if constexpr (kRounds) {
+        auto row = [&](const u32x4 v, uint32_t j) {
+            const H128 h = xxh3_16(((uint64_t)v.y << 32) | v.x, ((uint64_t)v.w << 32) | v.z);
+            W pw(md, h.lo, h.hi);
+            T m = all;
+#pragma unroll
+            for (int jj = 0; jj < K; jj++) {
+                m &= table[pw.pos()];
+                if (jj + 1 < K) pw.next(md);
+            }
+            __builtin_amdgcn_raw_buffer_store_b8(m, R.rsrc(out, j, 1), R.lane, 0, 0);
+        };
+        for (uint32_t j = 0; j < R.rounds; j += 3) {  // past the last round: empty windows (zeros, dropped rows)
+            row(ka, j);
+            __builtin_amdgcn_sched_barrier(0);
+            ka = round_keys(j + 3);
+            if (j + 1 == R.rounds) return;
+            row(kb, j + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            kb = round_keys(j + 4);
+            if (j + 2 == R.rounds) return;
+            row(kc, j + 2);
+            __builtin_amdgcn_sched_barrier(0);
+            kc = round_keys(j + 5);
+        }
+        return;
+    }
     const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     typename Src::Pre pre = src.fetch(i, i < n);  // next key's load is in flight while this one hashes
@@ -607,7 +689,8 @@ hipError_t probe_with(const Src& src, uint64_t n, const ProbeFilter* hf, uint32_
                     src, n, md, hf[0].k, nb, df, nfilt, stride, out);
             };
             const Mod32 m32 = hf[0].md;
-            const bool w32 = fits_walk32(nb), k7 = hf[0].k == 7;
+            // (the 1024-thread kernel counts its grid-wide rounds in 31 bits)
+            const bool w32 = fits_walk32(nb), k7 = hf[0].k == 7 && n < (1ull << 40);
             if (tsz == 1) {
                 if (k7 && std::is_same<Src, Fixed16>::value && Mod14::fits(nb))
                     go(k_probe_sliced<Src, uint8_t, Walk14, 7, 1024>, Mod14::make(nb), 1024);

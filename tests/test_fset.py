@@ -253,6 +253,58 @@ def test_fset_bounds_sharing_16_byte_prefixes(oracle):
     ctx.close()
 
 
+def _in_range16(rows, lo, hi):
+    """lo <= key <= hi for 16-byte keys (n x 16 uint8) in Rust [u8] order."""
+    def cmp(bound):  # -1 / 0 / 1 per row: key vs bound
+        b = np.frombuffer(bound[:16].ljust(16, b"\x00"), np.uint8)
+        d = rows.astype(np.int16) - b.astype(np.int16)
+        first = np.argmax(d != 0, axis=1)
+        c = np.sign(d[np.arange(rows.shape[0]), first]).astype(np.int8)
+        # equal first min(16, len) bytes: the shorter one orders first
+        eqp = np.all(rows[:, :min(16, len(bound))] == b[:min(16, len(bound))], axis=1)
+        c[eqp] = 0 if len(bound) == 16 else (1 if len(bound) < 16 else -1)
+        return c
+    return (cmp(lo) >= 0) & (cmp(hi) <= 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("q", [70_001, 524_289, 1_310_731])
+def test_fset_sliced_round_counts_and_long_bounds(oracle, q):
+    """The C3-shaped filter-set kernel (16-B keys, new(1000, .01) tables) over
+    several grid-strides and a partial last one; bounds longer than 16 bytes
+    that share a key's first 16 take the full byte compare, which re-reads
+    that key from memory."""
+    import torch
+
+    ctx = lsmbloom.Context(0)
+    fs = FilterSet(ctx)
+    nb, k = lsmbloom.params(1000, 0.01)
+    members = [keygen.key16(0x5EED0700 + t, 0, 1000) for t in range(8)]
+    keys = np.concatenate([keygen.key16(0x5EED0800, 0, q - q // 2)]
+                          + [members[t][np.random.default_rng(t).integers(0, 1000, q // 2 // 8 + 1)] for t in range(8)])[:q]
+    k0, k1 = bytes(keys[5]), bytes(keys[q // 2 + 3])
+    tables = {}
+    for t in range(8):
+        rows = sorted(bytes(r) for r in members[t])
+        lo, hi = [(rows[0], rows[-1]), (k0 + b"\x00", b"\xff" * 20), (k0[:15], k0 + b"\x07"),
+                  (b"", k1 + b"\x00\x01"), (k1, k1), (rows[100], rows[900]), (k0 + b"a" * 8, k1 + b"b" * 5),
+                  (b"\x00" * 17, b"\xff" * 16)][t]
+        w = oracle.build_fixed(members[t], 16, nb, k)
+        s = fs.add_filter(BloomFilter(w, k, nb), lo, hi)
+        tables[s] = (w, lo, hi)
+    exp = np.zeros(q, np.uint64)
+    for s, (w, lo, hi) in tables.items():
+        hit = oracle.probe([(w, nb, k)], keys, key_len=16)[:, 0].astype(bool)
+        exp |= (hit & _in_range16(keys, lo, hi)).astype(np.uint64) << np.uint64(s)
+    dq = torch.from_numpy(np.ascontiguousarray(keys)).to("cuda:0")
+    dout = torch.zeros(q, dtype=torch.int64, device="cuda:0")
+    fs.probe_dev(dq, q, dout, key_len=16)
+    torch.cuda.synchronize()
+    assert np.array_equal(dout.cpu().numpy().view(np.uint64), exp)
+    fs.close()
+    ctx.close()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("mixed", [False, True])
 def test_fset_random_ranges_region_lookup(oracle, mixed):

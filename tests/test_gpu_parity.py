@@ -315,7 +315,7 @@ def test_build_any_k(ctx, oracle, k):
 
 # ---------------------------------------------------------------- probe
 def _c3_filters(oracle, nfilt=8, members=1000):
-    nb, k = lsmbloom.params(1000, 0.01)  # SSTableBuilder::new sizing
+    nb, k = lsmbloom.params(members, 0.01)  # SSTableBuilder::new sizing at 1000
     fl, mem = [], []
     for f in range(nfilt):
         keys = keygen.key16(0xF000 + f, 0, members)
@@ -335,6 +335,19 @@ def test_probe_sliced_vs_oracle(ctx, oracle, nfilt):
     got = ctx.probe(fl, keys, key_len=16)
     ref = oracle.probe(fl, keys, key_len=16)
     assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("q,members", [(1, 1000), (63, 1000), (1025, 1000), (262_149, 1000), (786_532, 1000),
+                                       (1_048_577, 1000), (1_310_720, 1000), (1_048_577, 5000)])
+def test_probe_sliced_round_counts(ctx, oracle, q, members):
+    """The C3 kernel walks the keys in grid-wide rounds (256 CUs x 1024 lanes
+    on an MI355X), three in flight: one to five rounds, partial last rounds,
+    and a batch smaller than one workgroup; new(5000, .01) filters (47 836
+    bits, above Walk14's 2^14) take the same loop with the 32-bit walk."""
+    fl, mem = _c3_filters(oracle, 8, members)
+    rng = np.random.default_rng(q)
+    keys = np.concatenate([keygen.key16(0xABCD, 0, q - q // 2), mem[rng.integers(0, mem.shape[0], q // 2)]])
+    assert np.array_equal(ctx.probe(fl, keys, key_len=16), oracle.probe(fl, keys, key_len=16))
 
 
 def test_probe_generic_mixed_filters(ctx, oracle):
