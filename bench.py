@@ -966,12 +966,31 @@ class ProbeLegs:
         self.fsm.close()
 
 
-def timed_ms(fn, warmup, steps):
-    """Average ms of fn() over `steps` calls (HIP events on the current stream)."""
+def timed_ms(fn, warmup, steps, warm_ms=0.0, min_timed_ms=0.0):
+    """Average ms of fn() over `steps` calls (HIP events on the current stream).
+    warm_ms / min_timed_ms: keep warming up until that much device time has
+    run, and time at least that many ms of calls: a ~50 us probe needs ~20 ms
+    of back-to-back work before the GPU's clock has ramped (rocprofv3: the
+    C3 kernel takes 50 us in the first calls, 45.7 us from about the third
+    ms on), which the legs' few warmup calls do not give it."""
+    import time
+
     import torch
     for _ in range(max(1, warmup)):
         fn()
     torch.cuda.synchronize()
+    if warm_ms > 0:
+        t0 = time.perf_counter()
+        while (time.perf_counter() - t0) * 1e3 < warm_ms:
+            for _ in range(8):
+                fn()
+            torch.cuda.synchronize()
+    if min_timed_ms > 0:
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        one = max((time.perf_counter() - t0) * 1e3, 1e-3)
+        steps = max(steps, int(min_timed_ms / one) + 1)
     st = torch.cuda.Event(enable_timing=True)
     en = torch.cuda.Event(enable_timing=True)
     st.record()
@@ -992,7 +1011,7 @@ def bench_probe(ctx, dev, args, world=1, rank=0, max_over_ranks=lambda x: x):
     F, Q_all = args.probe_filters, args.probe_keys
     Q = Q_all // world
     P = ProbeLegs(ctx, dev, Q, F)
-    ms = max_over_ranks(timed_ms(P.probe, args.warmup, args.steps))
+    ms = max_over_ranks(timed_ms(P.probe, args.warmup, args.steps, warm_ms=20, min_timed_ms=10))
     alg = P.alg_bytes("probe")
     hits = int((P.out[: Q // 2] != 0).all(dim=1).sum().item())
     res = {"workload": "C3 (configs[2]): %d 16-B keys x %d filters new(1000, 0.01) (%d bits, k=%d)%s"
@@ -1009,7 +1028,7 @@ def bench_probe(ctx, dev, args, world=1, rank=0, max_over_ranks=lambda x: x):
     # The same batch through the device-resident filter set (lsmb_fset): per
     # key and SSTable, min_key <= key <= max_key && may_contain — the checks
     # SSTable::get makes (src/sstable/reader.rs:192-199) — for all 8 tables.
-    fms = max_over_ranks(timed_ms(P.fset, args.warmup, args.steps))
+    fms = max_over_ranks(timed_ms(P.fset, args.warmup, args.steps, warm_ms=20, min_timed_ms=10))
     # a member row's own table must answer 1 (range and bloom); here sel // 1000
     own = (P.fout[: Q // 2] >> torch.tensor(P.slots, device=dev)[P.sel // 1000]) & 1
     res["fset"] = {"what": "lsmb_fset_probe_dev: range pre-check + bloom, %d tables, u64 mask per key" % F,
@@ -1019,7 +1038,7 @@ def bench_probe(ctx, dev, args, world=1, rank=0, max_over_ranks=lambda x: x):
                                             "k_fset_sliced")}
     if c3fx and c3fx["Q"] == Q and c3fx["F"] == F:
         res["fset"]["answers_equal_oracle_fixture"] = _sha(P.fout) == c3fx["fset_mask_sha256"]
-    mms = max_over_ranks(timed_ms(P.fset_mixed, args.warmup, args.steps))
+    mms = max_over_ranks(timed_ms(P.fset_mixed, args.warmup, args.steps, warm_ms=20, min_timed_ms=10))
     res["fset_mixed"] = {"what": "lsmb_fset_probe_dev, %d tables of two sizes: %d x new(1000, 0.01) + %d x "
                                  "new(4000, 0.01), one LDS table per size class" % (F, F // 2, F - F // 2),
                          "value": round(Q * world / (mms * 1e-3) / 1e6, 2), "unit": "Mkeys/s", "ms": round(mms, 4),

@@ -49,6 +49,15 @@ __device__ __forceinline__ void store_row(uint8_t* out, uint64_t i, uint32_t str
     }
 }
 
+// The bit-sliced probe's filters, passed by value in the kernel arguments:
+// the kernel reads them with scalar loads at launch instead of chasing a
+// device descriptor array, and lsmb_probe then needs no descriptor upload
+// (nor the event that guards its reuse) for this path.
+struct SlicedFilters {
+    const uint32_t* w[32];  // filter f's words (LE u32 view of the u64 words)
+    uint32_t ob[32];        // filter f's output bit
+};
+
 // Grid-wide rounds over n items for the 1024-thread C3 probe: round j is
 // items [j*gs, (j+1)*gs), lane L of the grid takes item j*gs + L.  Each
 // round's keys and rows are addressed through a buffer resource whose base
@@ -85,8 +94,7 @@ struct Rounds {
 // workgroups, two per CU, so a CU builds it twice instead of eight times.
 template <class Src, typename T, class W, int K, int BS = 256>
 __global__ __launch_bounds__(BS) void k_probe_sliced(Src src, uint64_t n, typename W::Mod md, uint32_t k_,
-                                                      uint32_t num_bits,
-                                                      const ProbeFilter* __restrict__ filters,
+                                                      uint32_t num_bits, const SlicedFilters sf,
                                                       uint32_t nfilt, uint32_t stride,
                                                       uint8_t* __restrict__ out) {
     // 1024-thread instantiations (the hot 16-B-key / k = 7 ones) hold the
@@ -135,11 +143,34 @@ __global__ __launch_bounds__(BS) void k_probe_sliced(Src src, uint64_t n, typena
 #pragma unroll
     for (uint32_t f = 0; f < FMAX; f++) {
         const uint32_t g = f < nfilt ? f : 0u;
-        wp[f] = filters[g].words32;
-        ob[f] = filters[g].out_bit;
+        wp[f] = sf.w[g];
+        ob[f] = sf.ob[g];
         vm[f] = f < nfilt ? 1u : 0u;
     }
-    for (uint32_t w = threadIdx.x; w < nw32; w += blockDim.x) {
+    // One-byte entries with filter f on bit f (the probe's own layout): each
+    // (word, byte) item is an 8x8 bit transpose of the filters' bytes, three
+    // masked delta swaps on a u64, spread over all 1024 threads (a per-word
+    // loop of 32 x 8 bit extracts ran on 299 threads: ~900 VALU each).
+    bool ident = sizeof(T) == 1;
+#pragma unroll
+    for (uint32_t f = 0; f < FMAX; f++) ident = ident && ob[f] == f;
+    if (ident) {
+        for (uint32_t it = threadIdx.x; it < 4 * nw32; it += blockDim.x) {
+            const uint32_t w = it >> 2, sh = 8 * (it & 3);
+            uint64_t x = 0;
+#pragma unroll
+            for (uint32_t f = 0; f < FMAX; f++) x |= (uint64_t)((wp[f][w] >> sh) & (0xFFu * vm[f])) << (8 * f);
+            // row f, column i (filter f's bit 8 (it&3) + i) -> row i, column f
+            uint64_t t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;
+            x ^= t ^ (t << 7);
+            t = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull;
+            x ^= t ^ (t << 14);
+            t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull;
+            x ^= t ^ (t << 28);
+            *reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(table) + 8 * it) = x;
+        }
+    }
+    for (uint32_t w = threadIdx.x; !ident && w < nw32; w += blockDim.x) {
         uint32_t xs[FMAX];
 #pragma unroll
         for (uint32_t f = 0; f < FMAX; f++) xs[f] = wp[f][w];
@@ -156,7 +187,7 @@ __global__ __launch_bounds__(BS) void k_probe_sliced(Src src, uint64_t n, typena
     }
     __syncthreads();
     T all = 0;
-    for (uint32_t f = 0; f < nfilt; f++) all |= (T)((T)1 << filters[f].out_bit);
+    for (uint32_t f = 0; f < nfilt; f++) all |= (T)((T)1 << sf.ob[f]);
     if constexpr (kRounds) {
         auto row = [&](const u32x4 v, uint32_t j) {
             const H128 h = xxh3_16(((uint64_t)v.y << 32) | v.x, ((uint64_t)v.w << 32) | v.z);
@@ -664,29 +695,42 @@ hipError_t fset_probe_with(const Src& src, uint64_t n, const RangedFilter* df, u
     return hipGetLastError();
 }
 
+// Bytes of the bit-sliced LDS table the probe of these filters builds (all
+// share (num_bits, k), at most 32, the table within kProbeTableBytes), or 0
+// when they are walked from L2 by k_probe_generic instead.
+size_t sliced_bytes(const ProbeFilter* hf, uint32_t nfilt) {
+    bool same = nfilt > 0 && nfilt <= 32 && hf[0].k > 0;
+    for (uint32_t f = 1; f < nfilt && same; f++) same = hf[f].num_bits == hf[0].num_bits && hf[f].k == hf[0].k;
+    if (!same) return 0;
+    const size_t ent = (size_t)(((uint64_t)hf[0].num_bits + 31) / 32) * 32;  // 64-bit: nb + 31 wraps at 2^32-1
+    const size_t smem = ent * (nfilt <= 8 ? 1 : nfilt <= 16 ? 2 : 4);
+    return smem <= kProbeTableBytes ? smem : 0;
+}
+
 template <class Src>
 hipError_t probe_with(const Src& src, uint64_t n, const ProbeFilter* hf, uint32_t nfilt,
                       const ProbeFilter* df, uint8_t* out, int num_cus, hipStream_t st) {
     const uint32_t stride = (nfilt + 7) / 8;
-    bool same = nfilt > 0 && hf[0].k > 0;
-    for (uint32_t f = 1; f < nfilt && same; f++)
-        same = hf[f].num_bits == hf[0].num_bits && hf[f].k == hf[0].k;
     uint64_t g = (n + 255) / 256;
     const uint64_t gmax = (uint64_t)num_cus * 8;
     if (g > gmax) g = gmax;
     if (g < 1) g = 1;
-    if (same && nfilt <= 32) {
+    {
+        const size_t smem = sliced_bytes(hf, nfilt);
         const uint32_t nb = hf[0].num_bits;
-        const size_t ent = (size_t)(((uint64_t)nb + 31) / 32) * 32;  // 64-bit: nb + 31 wraps at 2^32-1
         const size_t tsz = nfilt <= 8 ? 1 : nfilt <= 16 ? 2 : 4;
-        const size_t smem = ent * tsz;
-        if (smem <= kProbeTableBytes) {
+        if (smem) {
+            SlicedFilters sf{};
+            for (uint32_t f = 0; f < nfilt; f++) {
+                sf.w[f] = hf[f].words32;
+                sf.ob[f] = hf[f].out_bit;
+            }
             auto go = [&](auto kern, auto md, uint32_t bs = 256) {
                 if (bs != 1024)  // (the 1024-thread kernels' table is static LDS)
                     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
                 const uint64_t gb = bs == 256 ? g : std::min<uint64_t>((n + bs - 1) / bs, probe_wgs_per_cu(1) * num_cus);
                 kern<<<dim3((uint32_t)std::max<uint64_t>(gb, 1)), dim3(bs), bs == 1024 ? 0 : smem, st>>>(
-                    src, n, md, hf[0].k, nb, df, nfilt, stride, out);
+                    src, n, md, hf[0].k, nb, sf, nfilt, stride, out);
             };
             const Mod32 m32 = hf[0].md;
             // (the 1024-thread kernel counts its grid-wide rounds in 31 bits)
@@ -729,6 +773,8 @@ hipError_t launch_fset_probe(const KeyBatch& kb, const RangedFilter* df, uint32_
     return fset_probe_with(FixedN{kb.data, kb.key_len}, kb.n, df, nfilt, rg, cl, shared_nb, shared_k, out, num_cus,
                            st);
 }
+
+bool probe_reads_descriptors(const ProbeFilter* hf, uint32_t nfilt) { return sliced_bytes(hf, nfilt) == 0; }
 
 hipError_t launch_probe(const KeyBatch& kb, const ProbeFilter* hf, uint32_t nfilt,
                         ProbeFilter* df, uint8_t* out, int num_cus, hipStream_t st) {

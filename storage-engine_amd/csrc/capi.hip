@@ -825,6 +825,13 @@ static int probe_common(lsmb_ctx* c, const uint32_t* const* wptrs, const uint32_
         p.out_bit = f;
         p.group = f;
     }
+    // The bit-sliced kernels (filters sharing one size, the store's SST
+    // filters) take the filters in their kernel arguments: nothing to upload
+    // and no event to record, so back-to-back probes are back-to-back kernels.
+    if (!probe_reads_descriptors(c->hfilt.data(), nfilt)) {
+        HIP_TRY(launch_probe(kb, c->hfilt.data(), nfilt, nullptr, d_out, c->num_cus, st));
+        return LSMB_OK;
+    }
     // Descriptors go to the device only when they change (a probe loop over the
     // same level filters re-uses them); the upload waits for the last kernel
     // that read the previous set, so no host sync sits between repeat probes.

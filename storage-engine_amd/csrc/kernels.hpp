@@ -187,6 +187,11 @@ hipError_t launch_fset_probe(const KeyBatch& kb, const RangedFilter* d_filters, 
                              const FsetClasses& cl, uint32_t shared_nb, uint32_t shared_k, uint64_t* d_out,
                              int num_cus, hipStream_t st);
 
+// True when launch_probe walks these filters with k_probe_generic, the one
+// probe kernel that reads the device descriptor copy (the bit-sliced kernels
+// take the filters in their arguments).
+bool probe_reads_descriptors(const ProbeFilter* h_filters, uint32_t nfilt);
+
 hipError_t launch_probe(const KeyBatch& kb, const ProbeFilter* h_filters, uint32_t nfilt,
                         ProbeFilter* d_filters_scratch, uint8_t* d_out, int num_cus,
                         hipStream_t st);
