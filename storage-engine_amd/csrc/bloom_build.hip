@@ -843,11 +843,14 @@ void launch_hash_var(const VarLen& src, uint64_t n, Out out, hipStream_t st) {
 template <class Src>
 hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k, uint32_t* gw,
                       BuildStrategy s, const PartitionWorkspace& ws, int num_cus, hipStream_t st,
-                      BuildTimers* tm, int sweep, bool fresh, bool t0_done = false) {
+                      BuildTimers* tm, int sweep, bool fresh, bool t0_done = false, hipEvent_t done = nullptr) {
+    // `done` is completed by the last kernel's own dispatch where the path ends
+    // in one (launch_done); otherwise recorded after it.
+    bool done_set = false;
     const Mod32 md = Mod32::make(num_bits);
     // sweep >= 0 (partition builds): only that sweep's slices — pass A keeps
     // their positions, pass B applies them; every other strategy has one sweep
-    if (sweep > 0 && s != BuildStrategy::Partition) return hipSuccess;
+    if (sweep > 0 && s != BuildStrategy::Partition) return done ? hipEventRecord(done, st) : hipSuccess;
     const uint32_t nw32 = (uint32_t)(2 * (((uint64_t)num_bits + 63) / 64));
     if (tm && !t0_done) hipEventRecord(tm->t0, st);
     constexpr bool kRecSrc = std::is_same<Src, ks::Recs>::value;  // walk records: partition builds only
@@ -893,8 +896,9 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
                 src, n, md, k, tp.nslices, nw32, tp.stride32, tiles);
         }
         if (tm) hipEventRecord(tm->t1, st);
-        hipError_t e = launch_or_reduce(gw, tiles, nw32, tp.chunks, tp.stride32, st);
+        hipError_t e = launch_or_reduce(gw, tiles, nw32, tp.chunks, tp.stride32, st, done);
         if (e != hipSuccess) return e;
+        done_set = done != nullptr;
     } else if (s == BuildStrategy::Atomic) {
         uint64_t g = (n + 255) / 256;
         if (g > (uint64_t)num_cus * 8) g = (uint64_t)num_cus * 8;
@@ -914,7 +918,7 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
             k_hash<Src, OutRec><<<dim3((uint32_t)g), dim3(256), 0, st>>>(src, n, rec);
         // pass A's timer (t1) covers k_hash + k_bin
         return build_with(ks::Recs{reinterpret_cast<const uint32_t*>(ws.hashes)}, n, num_bits, k, gw, s, ws, num_cus,
-                          st, tm, sweep, fresh, /*t0_done=*/true);
+                          st, tm, sweep, fresh, /*t0_done=*/true, done);
     } else {
         const PartitionPlan pl = plan_partition(num_bits, k, n, num_cus);
         if (pl.region_bytes > ws.region_bytes || pl.counts_bytes > ws.counts_bytes) return hipErrorInvalidValue;
@@ -1015,20 +1019,26 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
         if (tm) hipEventRecord(tm->t1, st);
         if (bend > bfirst) {
             uint32_t* dmark = list ? ws.dirty : nullptr;
+            hipEvent_t apply_done = list ? nullptr : done;  // (the last kernel completes `done`)
+            hipError_t e;
             if (pl.slice_log2 == 21)
-                k_apply<21><<<dim3(2 * (bend - bfirst)), dim3(kApplyBlock), 0, st>>>(
-                    ws.regions, ws.counts, pl.grid, pl.cap_segs, pl.nbins, gw, nw32, bfirst, bend, ws.ovf, dmark, list);
+                e = launch_done(k_apply<21>, dim3(2 * (bend - bfirst)), dim3(kApplyBlock), 0u, st, apply_done, ws.regions,
+                                ws.counts, pl.grid, pl.cap_segs, pl.nbins, gw, nw32, bfirst, bend, ws.ovf, dmark, list);
             else
-                k_apply<<<dim3(bend - bfirst), dim3(kApplyBlock), 0, st>>>(ws.regions, ws.counts, pl.grid,
-                                                                           pl.cap_segs, pl.nbins, gw, nw32, bfirst,
-                                                                           bend, ws.ovf, dmark, list);
+                e = launch_done(k_apply<kSliceLog2>, dim3(bend - bfirst), dim3(kApplyBlock), 0u, st, apply_done, ws.regions,
+                                ws.counts, pl.grid, pl.cap_segs, pl.nbins, gw, nw32, bfirst, bend, ws.ovf, dmark, list);
+            if (e != hipSuccess) return e;
             if (list) {  // the lists of the sweeps this call ran
                 const uint32_t s0 = sweep >= 0 ? (uint32_t)sweep : 0u, ns = sweep >= 0 ? 1u : pl.sweeps;
-                k_ovf_apply<<<dim3(ns * pl.grid), dim3(256), 0, st>>>(ws.ovl + (uint64_t)s0 * pl.grid * kOvfListCap,
-                                                                      ws.ovn + (uint64_t)s0 * pl.grid, kOvfListCap, gw);
+                e = launch_done(k_ovf_apply, dim3(ns * pl.grid), dim3(256), 0u, st, done,
+                                (const uint32_t*)(ws.ovl + (uint64_t)s0 * pl.grid * kOvfListCap),
+                                (const uint32_t*)(ws.ovn + (uint64_t)s0 * pl.grid), (uint32_t)kOvfListCap, gw);
+                if (e != hipSuccess) return e;
             }
+            done_set = done != nullptr;
         }
     }
+    if (done && !done_set) hipEventRecord(done, st);
     if (tm) {
         hipEventRecord(tm->t2, st);
         tm->valid = true;
@@ -1176,26 +1186,28 @@ uint64_t partition_chunk_keys(uint32_t num_bits, uint32_t k, uint64_t max_bytes,
 
 hipError_t launch_build(const KeyBatch& kb, uint32_t num_bits, uint32_t k, uint32_t* gw,
                         BuildStrategy s, const PartitionWorkspace& ws, int num_cus, hipStream_t st,
-                        BuildTimers* tm, int sweep, bool fresh) {
+                        BuildTimers* tm, int sweep, bool fresh, hipEvent_t done) {
     if (s == BuildStrategy::None) {
-        if (!fresh || num_bits == 0) return hipSuccess;
-        return hipMemsetAsync(gw, 0, (size_t)(((uint64_t)num_bits + 63) / 64) * 8, st);  // new(), no inserts
+        if (fresh && num_bits) {
+            const hipError_t e = hipMemsetAsync(gw, 0, (size_t)(((uint64_t)num_bits + 63) / 64) * 8, st);  // new(), no inserts
+            if (e != hipSuccess) return e;
+        }
+        return done ? hipEventRecord(done, st) : hipSuccess;
     }
     if (kb.offsets)
-        return build_with(VarLen{kb.data, kb.offsets}, kb.n, num_bits, k, gw, s, ws, num_cus, st, tm, sweep, fresh);
+        return build_with(VarLen{kb.data, kb.offsets}, kb.n, num_bits, k, gw, s, ws, num_cus, st, tm, sweep, fresh, false, done);
     if (kb.key_len == 16 && (reinterpret_cast<uintptr_t>(kb.data) & 15) == 0)
         return build_with(Fixed16{reinterpret_cast<const uint4*>(kb.data)}, kb.n, num_bits, k, gw, s, ws,
-                          num_cus, st, tm, sweep, fresh);
-    return build_with(FixedN{kb.data, kb.key_len}, kb.n, num_bits, k, gw, s, ws, num_cus, st, tm, sweep, fresh);
+                          num_cus, st, tm, sweep, fresh, false, done);
+    return build_with(FixedN{kb.data, kb.key_len}, kb.n, num_bits, k, gw, s, ws, num_cus, st, tm, sweep, fresh, false, done);
 }
 
 hipError_t launch_or_reduce(uint32_t* dst, const uint32_t* src, uint64_t nw32, uint32_t nsrc,
-                            uint64_t stride32, hipStream_t st) {
+                            uint64_t stride32, hipStream_t st, hipEvent_t done) {
     uint64_t g = (nw32 + 255) / 256;
     if (g > 8192) g = 8192;
     if (g < 1) g = 1;
-    k_or_reduce<<<dim3((uint32_t)g), dim3(256), 0, st>>>(dst, src, nw32, nsrc, stride32);
-    return hipGetLastError();
+    return launch_done(k_or_reduce, dim3((uint32_t)g), dim3(256), 0u, st, done, dst, src, nw32, nsrc, stride32);
 }
 
 hipError_t launch_gen_key16(uint64_t seed, uint64_t first, uint64_t n, uint8_t* d_keys, hipStream_t st) {

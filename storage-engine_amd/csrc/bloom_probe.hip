@@ -652,7 +652,7 @@ uint64_t probe_wgs_per_cu(uint64_t dflt) {
 template <class Src>
 hipError_t fset_probe_with(const Src& src, uint64_t n, const RangedFilter* df, uint32_t nfilt, const FsetRanges& rg,
                            const FsetClasses& cl, uint32_t shared_nb, uint32_t shared_k, uint64_t* out, int num_cus,
-                           hipStream_t st) {
+                           hipStream_t st, hipEvent_t done) {
     uint64_t g = (n + 255) / 256;
     const uint64_t gmax = (uint64_t)num_cus * 8;
     if (g > gmax) g = gmax;
@@ -663,8 +663,8 @@ hipError_t fset_probe_with(const Src& src, uint64_t n, const RangedFilter* df, u
         if (gc > (uint64_t)num_cus * class_wgs_per_cu<Src>()) gc = (uint64_t)num_cus * class_wgs_per_cu<Src>();
         if (gc < 1) gc = 1;
         hipFuncSetAttribute((const void*)k_fset_classes<Src>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-        k_fset_classes<Src><<<dim3((uint32_t)gc), dim3(kClassBlock), smem, st>>>(src, n, df, nfilt, rg, cl, out);
-        return hipGetLastError();
+        return launch_done(k_fset_classes<Src>, dim3((uint32_t)gc), dim3(kClassBlock), (uint32_t)smem, st, done, src, n, df,
+                           nfilt, rg, cl, out);
     }
     if (shared_nb > 0 && shared_k > 0) {
         const size_t tsz = nfilt <= 8 ? 1 : nfilt <= 16 ? 2 : nfilt <= 32 ? 4 : 8;
@@ -675,8 +675,8 @@ hipError_t fset_probe_with(const Src& src, uint64_t n, const RangedFilter* df, u
                 if (bs != 1024)  // (the 1024-thread kernels' table is static LDS)
                     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
                 const uint64_t gb = bs == 256 ? g : std::min<uint64_t>((n + bs - 1) / bs, probe_wgs_per_cu(2) * num_cus);
-                kern<<<dim3((uint32_t)std::max<uint64_t>(gb, 1)), dim3(bs), bs == 1024 ? 0 : smem, st>>>(
-                    src, n, df, nfilt, rg, shared_k, md, out);
+                launch_done(kern, dim3((uint32_t)std::max<uint64_t>(gb, 1)), dim3(bs), bs == 1024 ? 0u : (uint32_t)smem, st,
+                            done, src, n, df, nfilt, rg, shared_k, md, out);
             };
             if (tsz == 1) {
                 if (shared_k == 7 && std::is_same<Src, Fixed16>::value && Mod14::fits(shared_nb))
@@ -691,8 +691,7 @@ hipError_t fset_probe_with(const Src& src, uint64_t n, const RangedFilter* df, u
             return hipGetLastError();
         }
     }
-    k_fset_probe<Src><<<dim3((uint32_t)g), dim3(256), 0, st>>>(src, n, df, nfilt, rg, out);
-    return hipGetLastError();
+    return launch_done(k_fset_probe<Src>, dim3((uint32_t)g), dim3(256), 0u, st, done, src, n, df, nfilt, rg, out);
 }
 
 // Bytes of the bit-sliced LDS table the probe of these filters builds (all
@@ -709,7 +708,7 @@ size_t sliced_bytes(const ProbeFilter* hf, uint32_t nfilt) {
 
 template <class Src>
 hipError_t probe_with(const Src& src, uint64_t n, const ProbeFilter* hf, uint32_t nfilt,
-                      const ProbeFilter* df, uint8_t* out, int num_cus, hipStream_t st) {
+                      const ProbeFilter* df, uint8_t* out, int num_cus, hipStream_t st, hipEvent_t done) {
     const uint32_t stride = (nfilt + 7) / 8;
     uint64_t g = (n + 255) / 256;
     const uint64_t gmax = (uint64_t)num_cus * 8;
@@ -753,37 +752,36 @@ hipError_t probe_with(const Src& src, uint64_t n, const ProbeFilter* hf, uint32_
             return hipGetLastError();
         }
     }
-    k_probe_generic<Src><<<dim3((uint32_t)g), dim3(256), 0, st>>>(src, n, df, nfilt, stride, out);
-    return hipGetLastError();
+    return launch_done(k_probe_generic<Src>, dim3((uint32_t)g), dim3(256), 0u, st, done, src, n, df, nfilt, stride, out);
 }
 
 }  // namespace
 
 hipError_t launch_fset_probe(const KeyBatch& kb, const RangedFilter* df, uint32_t nfilt, const FsetRanges& rg,
                              const FsetClasses& cl, uint32_t shared_nb, uint32_t shared_k, uint64_t* out, int num_cus,
-                             hipStream_t st) {
+                             hipStream_t st, hipEvent_t done) {
     if (kb.n == 0) return hipSuccess;
     if (nfilt > 64 || rg.npts > kFsetMaxPoints || cl.ncls > kFsetMaxClasses) return hipErrorInvalidValue;
     if (kb.offsets)
         return fset_probe_with(VarLen{kb.data, kb.offsets}, kb.n, df, nfilt, rg, cl, shared_nb, shared_k, out, num_cus,
-                               st);
+                               st, done);
     if (kb.key_len == 16 && (reinterpret_cast<uintptr_t>(kb.data) & 15) == 0)
         return fset_probe_with(Fixed16{reinterpret_cast<const uint4*>(kb.data)}, kb.n, df, nfilt, rg, cl, shared_nb,
-                               shared_k, out, num_cus, st);
+                               shared_k, out, num_cus, st, done);
     return fset_probe_with(FixedN{kb.data, kb.key_len}, kb.n, df, nfilt, rg, cl, shared_nb, shared_k, out, num_cus,
-                           st);
+                           st, done);
 }
 
 bool probe_reads_descriptors(const ProbeFilter* hf, uint32_t nfilt) { return sliced_bytes(hf, nfilt) == 0; }
 
 hipError_t launch_probe(const KeyBatch& kb, const ProbeFilter* hf, uint32_t nfilt,
-                        ProbeFilter* df, uint8_t* out, int num_cus, hipStream_t st) {
+                        ProbeFilter* df, uint8_t* out, int num_cus, hipStream_t st, hipEvent_t done) {
     if (kb.n == 0) return hipSuccess;
-    if (kb.offsets) return probe_with(VarLen{kb.data, kb.offsets}, kb.n, hf, nfilt, df, out, num_cus, st);
+    if (kb.offsets) return probe_with(VarLen{kb.data, kb.offsets}, kb.n, hf, nfilt, df, out, num_cus, st, done);
     if (kb.key_len == 16 && (reinterpret_cast<uintptr_t>(kb.data) & 15) == 0)
         return probe_with(Fixed16{reinterpret_cast<const uint4*>(kb.data)}, kb.n, hf, nfilt, df, out,
-                          num_cus, st);
-    return probe_with(FixedN{kb.data, kb.key_len}, kb.n, hf, nfilt, df, out, num_cus, st);
+                          num_cus, st, done);
+    return probe_with(FixedN{kb.data, kb.key_len}, kb.n, hf, nfilt, df, out, num_cus, st, done);
 }
 
 }  // namespace lsmb

@@ -96,7 +96,7 @@ void report_stats(lsmb_ctx* c) {
 
 namespace {
 int build_dev_ws(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k, uint32_t* dw, hipStream_t st,
-                 BuildStrategy s, int sweep, bool fresh);
+                 BuildStrategy s, int sweep, bool fresh, hipEvent_t done = nullptr);
 }  // namespace
 
 // Device build of one batch, chunked so the partition workspace stays bounded.
@@ -119,16 +119,19 @@ int build_dev(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k
     // streams' builds would otherwise overwrite each other's regions).  On the
     // same stream, stream order already serialises them: no wait packet (a
     // barrier packet between consecutive builds costs the stream ~10 us).
+    // ws_done is completed by the build's last kernel itself (launch_done): a
+    // separate event record would put a marker packet, ~6 us, between
+    // back-to-back builds.
     if (c->ws_stream && c->ws_stream != st) HIP_TRY(hipStreamWaitEvent(st, c->ws_done, 0));
-    const int rc = build_dev_ws(c, kb_all, num_bits, k, dw, st, s, sweep, fresh);
-    HIP_TRY(hipEventRecord(c->ws_done, st));
+    const int rc = build_dev_ws(c, kb_all, num_bits, k, dw, st, s, sweep, fresh, c->ws_done);
+    if (rc != LSMB_OK) HIP_TRY(hipEventRecord(c->ws_done, st));  // (a failed build may have launched nothing)
     c->ws_stream = st;
     return rc;
 }
 
 namespace {
 int build_dev_ws(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_t k, uint32_t* dw, hipStream_t st,
-                 BuildStrategy s, int sweep, bool fresh) {
+                 BuildStrategy s, int sweep, bool fresh, hipEvent_t done) {
     if (s == BuildStrategy::Tiled) {
         const TiledPlan tp = plan_tiled(num_bits, kb_all.n, c->num_cus);
         HIP_TRY(c->ws_regions.ensure(tp.scratch_bytes));
@@ -141,12 +144,12 @@ int build_dev_ws(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_
             ws.hash_bytes = c->ws_hashes.bytes;
         }
         HIP_TRY(launch_build(kb_all, num_bits, k, dw, s, ws, c->num_cus, st, c->timing ? &c->tm : nullptr, sweep,
-                             fresh));
+                             fresh, done));
         return LSMB_OK;
     }
     if (s != BuildStrategy::Partition) {
         HIP_TRY(launch_build(kb_all, num_bits, k, dw, s, PartitionWorkspace{}, c->num_cus, st,
-                             c->timing ? &c->tm : nullptr, sweep, fresh));
+                             c->timing ? &c->tm : nullptr, sweep, fresh, done));
         return LSMB_OK;
     }
     uint64_t chunk = partition_chunk_keys(num_bits, k, workspace_limit_bytes(), c->num_cus);
@@ -196,7 +199,7 @@ int build_dev_ws(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_
             kb.data += first * kb.key_len;
         // fresh: the first chunk writes every word of the range, the rest accumulate
         HIP_TRY(launch_build(kb, num_bits, k, dw, s, ws, c->num_cus, st, c->timing ? &c->tm : nullptr, sweep,
-                             fresh && first == 0));
+                             fresh && first == 0, done));  // (each chunk's last kernel re-arms `done`)
     }
     return LSMB_OK;
 }
@@ -825,6 +828,7 @@ static int probe_common(lsmb_ctx* c, const uint32_t* const* wptrs, const uint32_
         p.out_bit = f;
         p.group = f;
     }
+    if (kb.n == 0) return LSMB_OK;  // (no launch: nothing would complete the guard event below)
     // The bit-sliced kernels (filters sharing one size, the store's SST
     // filters) take the filters in their kernel arguments: nothing to upload
     // and no event to record, so back-to-back probes are back-to-back kernels.
@@ -846,8 +850,8 @@ static int probe_common(lsmb_ctx* c, const uint32_t* const* wptrs, const uint32_
                                hipMemcpyHostToDevice, st));
         c->desc_uploaded = c->hfilt;
     }
-    HIP_TRY(launch_probe(kb, c->hfilt.data(), nfilt, (ProbeFilter*)c->filt_desc.p, d_out, c->num_cus, st));
-    HIP_TRY(hipEventRecord(c->desc_done, st));
+    HIP_TRY(launch_probe(kb, c->hfilt.data(), nfilt, (ProbeFilter*)c->filt_desc.p, d_out, c->num_cus, st,
+                         c->desc_done));  // (the dispatch completes the guard event)
     return LSMB_OK;
 }
 
@@ -992,10 +996,15 @@ int fset_wait_probes(lsmb_fset* fs) {
 // whose probe the host waits for first.
 constexpr size_t kFsetProbeStreams = 4;
 
-int fset_note_probe(lsmb_fset* fs, hipStream_t st) {
+// The event that will mark the completion of the next probe on stream st
+// (the set's buffers are rewritten only after every probe that reads them
+// is done): one per stream, at most kFsetProbeStreams of them, the least
+// recently used evicted after a wait.  The probe's own dispatch completes it
+// (launch_done), so repeated probes put no marker packets in the stream.
+int fset_probe_event(lsmb_fset* fs, hipStream_t st, hipEvent_t* out) {
     for (size_t i = 0; i < fs->probe_ev.size(); i++)
         if (fs->probe_ev[i].first == st) {
-            HIP_TRY(hipEventRecord(fs->probe_ev[i].second, st));
+            *out = fs->probe_ev[i].second;
             std::rotate(fs->probe_ev.begin() + i, fs->probe_ev.begin() + i + 1, fs->probe_ev.end());  // most recent last
             return LSMB_OK;
         }
@@ -1008,7 +1017,7 @@ int fset_note_probe(lsmb_fset* fs, hipStream_t st) {
         fs->probe_ev.erase(fs->probe_ev.begin());
     }
     fs->probe_ev.push_back({st, ev});
-    HIP_TRY(hipEventRecord(ev, st));
+    *out = ev;
     return LSMB_OK;
 }
 
@@ -1274,9 +1283,11 @@ int lsmb_fset_probe_dev(lsmb_fset* fs, const void* d_data, const void* d_offsets
         return LSMB_OK;
     }
     KeyBatch kb{(const uint8_t*)d_data, (const uint64_t*)d_offsets, key_len, n};
+    hipEvent_t ev;
+    if (int rc = fset_probe_event(fs, st, &ev)) return rc;
     HIP_TRY(launch_fset_probe(kb, (const RangedFilter*)fs->desc.p, fs->ndesc, fs->rg, fs->cl, fs->shared_nb, fs->shared_k,
-                              (uint64_t*)d_out, fs->c->num_cus, st));
-    return fset_note_probe(fs, st);
+                              (uint64_t*)d_out, fs->c->num_cus, st, ev));
+    return LSMB_OK;
 }
 
 int lsmb_fset_probe(lsmb_fset* fs, const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
@@ -1295,9 +1306,10 @@ int lsmb_fset_probe(lsmb_fset* fs, const uint8_t* data, const uint64_t* offsets,
         memset(out_mask, 0, n * 8);
         return LSMB_OK;
     }
+    hipEvent_t ev;
+    if (int rc = fset_probe_event(fs, c->st, &ev)) return rc;
     HIP_TRY(launch_fset_probe(kb, (const RangedFilter*)fs->desc.p, fs->ndesc, fs->rg, fs->cl, fs->shared_nb, fs->shared_k,
-                              (uint64_t*)c->out.p, c->num_cus, c->st));
-    if (int rc = fset_note_probe(fs, c->st)) return rc;
+                              (uint64_t*)c->out.p, c->num_cus, c->st, ev));
     HIP_TRY(hipMemcpyAsync(out_mask, c->out.p, n * 8, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(hipStreamSynchronize(c->st));
     return LSMB_OK;

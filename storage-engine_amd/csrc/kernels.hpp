@@ -1,6 +1,7 @@
 // kernels.hpp — launchers for the Bloom build / probe kernels (internal).
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -117,7 +118,8 @@ struct BuildTimers {
 // build for the other strategies; see build_sweeps / sweep_words).
 hipError_t launch_build(const KeyBatch& kb, uint32_t num_bits, uint32_t k, uint32_t* d_words32,
                         BuildStrategy s, const PartitionWorkspace& ws, int num_cus,
-                        hipStream_t st, BuildTimers* timers, int sweep = -1, bool fresh = false);
+                        hipStream_t st, BuildTimers* timers, int sweep = -1, bool fresh = false,
+                        hipEvent_t done = nullptr);  // done: completed by the build's last kernel (launch_done)
 
 // Filter descriptor for the probe kernels (device-side array).
 struct ProbeFilter {
@@ -183,9 +185,23 @@ struct FsetClasses {
 // the nfilt (<= 64) descriptors at d_filters (device memory).  One class
 // holding every descriptor takes the bit-sliced kernel with a compile-time
 // entry width; several classes the per-class tables; none the L2 walk.
+// done (optional): an event the dispatch itself completes (see launch_done).
 hipError_t launch_fset_probe(const KeyBatch& kb, const RangedFilter* d_filters, uint32_t nfilt, const FsetRanges& rg,
                              const FsetClasses& cl, uint32_t shared_nb, uint32_t shared_k, uint64_t* d_out,
-                             int num_cus, hipStream_t st);
+                             int num_cus, hipStream_t st, hipEvent_t done = nullptr);
+
+// A kernel launch whose completion also completes `done` (when non-null):
+// hipExtLaunchKernelGGL tracks the event with the dispatch's own completion
+// signal, where hipEventRecord after the launch would put a marker packet in
+// the stream — ~6 us between back-to-back kernels (rocprofv3, the C3 probe).
+template <typename K, typename... Args>
+hipError_t launch_done(K kern, dim3 grid, dim3 block, uint32_t smem, hipStream_t st, hipEvent_t done, Args... args) {
+    if (done)
+        hipExtLaunchKernelGGL(kern, grid, block, smem, st, nullptr, done, 0, args...);
+    else
+        kern<<<grid, block, smem, st>>>(args...);
+    return hipGetLastError();
+}
 
 // True when launch_probe walks these filters with k_probe_generic, the one
 // probe kernel that reads the device descriptor copy (the bit-sliced kernels
@@ -194,10 +210,10 @@ bool probe_reads_descriptors(const ProbeFilter* h_filters, uint32_t nfilt);
 
 hipError_t launch_probe(const KeyBatch& kb, const ProbeFilter* h_filters, uint32_t nfilt,
                         ProbeFilter* d_filters_scratch, uint8_t* d_out, int num_cus,
-                        hipStream_t st);
+                        hipStream_t st, hipEvent_t done = nullptr);
 
 hipError_t launch_or_reduce(uint32_t* dst, const uint32_t* src, uint64_t nwords32, uint32_t nsrc,
-                            uint64_t stride32, hipStream_t st);
+                            uint64_t stride32, hipStream_t st, hipEvent_t done = nullptr);
 
 hipError_t launch_gen_splitmix(uint64_t seed, uint64_t first, uint64_t n, uint32_t mod, uint32_t add,
                                uint64_t* d_out, hipStream_t st);
