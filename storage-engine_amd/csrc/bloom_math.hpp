@@ -207,8 +207,13 @@ struct WalkRec {
 
     static LSMB_HD WalkRec make(const Mod32& md, const H128& h, uint32_t k) {
         WalkRec q;
-        q.r = md.reduce(h.lo);
-        q.s = md.reduce(h.hi);
+        if (md.d <= 0x80000000u) {  // (uniform) the 32-bit remainder path, as Walk32 takes
+            q.r = md.reduce31(h.lo);
+            q.s = md.reduce31(h.hi);
+        } else {
+            q.r = md.reduce(h.lo);
+            q.s = md.reduce(h.hi);
+        }
         q.c = 0;
         uint64_t x = h.lo;
         for (uint32_t i = 0; i + 1 < k && i < 31; i++) {

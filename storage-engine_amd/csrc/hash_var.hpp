@@ -8,22 +8,27 @@
 namespace lsmb {
 
 // Key bytes from a workgroup's LDS window (k_hash_var): LE loads at any byte
-// offset as funnel shifts of aligned dwords (the window has >= 12 B of slack).
+// offset (the window has >= 12 B of slack past its last byte).
 struct LdsReader {
     const uint32_t* w;
     uint32_t base;  // the key's first byte in the window
+    // Byte-aligned LDS loads: gfx950 kernels run in unaligned access mode, so
+    // the compiler emits one ds_read at any byte address, folds constant
+    // offsets into it and merges a 16-B run (mix32's a, a + 8) into one
+    // ds_read_b128.  Building each 8 B from aligned dwords with v_alignbit
+    // took ~5 VALU and 3 ds_read_b32 (k_hash_var: 2692 -> 2203 static VALU).
     __device__ __forceinline__ uint64_t ld64(uint64_t o) const {
-        const uint32_t a = base + (uint32_t)o, i = a >> 2, sh = (a & 3) * 8;
-        const uint32_t d0 = w[i], d1 = w[i + 1], d2 = w[i + 2];
-        return ((uint64_t)__builtin_amdgcn_alignbit(d2, d1, sh) << 32) | __builtin_amdgcn_alignbit(d1, d0, sh);
+        uint64_t v;
+        __builtin_memcpy(&v, reinterpret_cast<const uint8_t*>(w) + base + (uint32_t)o, 8);
+        return v;
     }
     __device__ __forceinline__ uint32_t ld32(uint64_t o) const {
-        const uint32_t a = base + (uint32_t)o, i = a >> 2, sh = (a & 3) * 8;
-        return __builtin_amdgcn_alignbit(w[i + 1], w[i], sh);
+        uint32_t v;
+        __builtin_memcpy(&v, reinterpret_cast<const uint8_t*>(w) + base + (uint32_t)o, 4);
+        return v;
     }
     __device__ __forceinline__ uint32_t u8(uint64_t o) const {
-        const uint32_t a = base + (uint32_t)o;
-        return (w[a >> 2] >> ((a & 3) * 8)) & 0xFFu;
+        return reinterpret_cast<const uint8_t*>(w)[base + (uint32_t)o];
     }
 };
 

@@ -193,8 +193,12 @@ LSMB_HD H128 len129to240(const R& r, uint32_t len) {
     for (int i = 0; i < 4; i++) mix32(acc, r, 32 * i, 32 * i + 16, 32 * i);
     acc.lo = aval3(acc.lo);
     acc.hi = aval3(acc.hi);
-    const uint32_t rounds = len >> 5;
-    for (uint32_t i = 4; i < rounds; i++) mix32(acc, r, 32 * i, 32 * i + 16, 3 + 32 * (int)(i - 4));
+    const uint32_t rounds = len >> 5;  // 4..7
+    // unrolled over the three possible extra rounds: the secret offsets are
+    // compile-time constants (immediates), not per-round loads
+#pragma unroll
+    for (uint32_t i = 4; i < 7; i++)
+        if (i < rounds) mix32(acc, r, 32 * i, 32 * i + 16, 3 + 32 * (int)(i - 4));
     mix32(acc, r, len - 16, len - 32, 136 - 17 - 16);
     return mid_finish(acc, len);
 }
