@@ -214,13 +214,30 @@ struct WalkRec {
             q.r = md.reduce(h.lo);
             q.s = md.reduce(h.hi);
         }
+        const uint32_t steps = k < 2 ? 0u : (k - 1 < 31 ? k - 1 : 31u);
+#ifdef __HIP_DEVICE_COMPILE__
+        // The carries through one add-with-carry chain: x += h2 leaves the
+        // carry in vcc, and acc = acc + acc + vcc shifts it in (3 VALU a step
+        // against ~5 for a 64-bit add, a compare and a select-or); the first
+        // carry lands in the top bit, so the bits are reversed at the end.
+        uint32_t lo = (uint32_t)h.lo, hi = (uint32_t)(h.lo >> 32), acc = 0;
+        const uint32_t dlo = (uint32_t)h.hi, dhi = (uint32_t)(h.hi >> 32);
+        for (uint32_t i = 0; i < steps; i++)
+            asm volatile("v_add_co_u32 %0, vcc, %0, %3\n\tv_addc_co_u32 %1, vcc, %1, %4, vcc\n\t"
+                         "v_addc_co_u32 %2, vcc, %2, %2, vcc"
+                         : "+v"(lo), "+v"(hi), "+v"(acc)
+                         : "v"(dlo), "v"(dhi)
+                         : "vcc");
+        q.c = steps ? __builtin_bitreverse32(acc) >> (32 - steps) : 0u;
+#else
         q.c = 0;
         uint64_t x = h.lo;
-        for (uint32_t i = 0; i + 1 < k && i < 31; i++) {
+        for (uint32_t i = 0; i < steps; i++) {
             uint64_t nx;
             if (__builtin_add_overflow(x, h.hi, &nx)) q.c |= 1u << i;
             x = nx;
         }
+#endif
         return q;
     }
 };
