@@ -456,7 +456,31 @@ __global__ __launch_bounds__(BS) void k_fset_sliced(Src src, uint64_t n, const R
     bool ident = true;  // slots 0..nfilt-1 all live: table bit f is output bit f
     for (uint32_t f = 0; f < nfilt; f++) ident = ident && fl[f].f.out_bit == f;
     const uint32_t nw32 = (num_bits + 31) / 32;  // num_bits <= 2^19 here: no wrap
-    for (uint32_t w = threadIdx.x; w < nw32; w += blockDim.x) {
+    if constexpr (sizeof(T) == 1) {
+        // one-byte entries (<= 8 tables): 8x8 bit transposes over all threads,
+        // as k_probe_sliced builds its table (absent slots: filter 0, masked)
+        const uint32_t* wp[8];
+        uint32_t vm[8];
+#pragma unroll
+        for (uint32_t f = 0; f < 8; f++) {
+            wp[f] = fl[f < nfilt ? f : 0].f.words32;
+            vm[f] = f < nfilt ? 0xFFu : 0u;
+        }
+        for (uint32_t it = threadIdx.x; it < 4 * nw32; it += blockDim.x) {
+            const uint32_t w = it >> 2, sh = 8 * (it & 3);
+            uint64_t x = 0;
+#pragma unroll
+            for (uint32_t f = 0; f < 8; f++) x |= (uint64_t)((wp[f][w] >> sh) & vm[f]) << (8 * f);
+            uint64_t t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;
+            x ^= t ^ (t << 7);
+            t = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull;
+            x ^= t ^ (t << 14);
+            t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull;
+            x ^= t ^ (t << 28);
+            *reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(table) + 8 * it) = x;
+        }
+    }
+    for (uint32_t w = threadIdx.x; sizeof(T) > 1 && w < nw32; w += blockDim.x) {
         T acc[32];
 #pragma unroll
         for (int b = 0; b < 32; b++) acc[b] = 0;
