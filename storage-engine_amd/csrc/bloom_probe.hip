@@ -555,6 +555,29 @@ __global__ __launch_bounds__(kClassBlock, 4 * class_wgs_per_cu<Src>()) void k_fs
     for (uint32_t c = 0; c < cl.ncls; c++) {
         const uint32_t nw32 = (C[c].num_bits + 31) / 32, nm = C[c].nmem, width = C[c].width;
         uint8_t* t = smem_raw + C[c].off;
+        if (width == 1) {  // (uniform) <= 8 members: 8x8 bit transposes over all threads, as k_fset_sliced
+            const uint32_t* wp[8];
+            uint32_t vm[8];
+#pragma unroll
+            for (uint32_t j = 0; j < 8; j++) {
+                wp[j] = fl[mem[c][j < nm ? j : 0]].f.words32;
+                vm[j] = j < nm ? 0xFFu : 0u;
+            }
+            for (uint32_t it = threadIdx.x; it < 4 * nw32; it += blockDim.x) {
+                const uint32_t w = it >> 2, sh = 8 * (it & 3);
+                uint64_t x = 0;
+#pragma unroll
+                for (uint32_t j = 0; j < 8; j++) x |= (uint64_t)((wp[j][w] >> sh) & vm[j]) << (8 * j);
+                uint64_t q = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;
+                x ^= q ^ (q << 7);
+                q = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull;
+                x ^= q ^ (q << 14);
+                q = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull;
+                x ^= q ^ (q << 28);
+                *reinterpret_cast<uint64_t*>(t + 8 * it) = x;
+            }
+            continue;
+        }
         for (uint32_t w = threadIdx.x; w < nw32; w += blockDim.x) {
             for (uint32_t j0 = 0; j0 < nm; j0 += 32) {
                 uint32_t acc[32];
