@@ -521,6 +521,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(nb, k, args.cpu_seconds)
         out["cpu_baseline"]["gpu_over_cpu_1thread"] = round(value / out["cpu_baseline"]["value"], 1)
     if rank == 0:
+        out["native"] = native_record()
         print(json.dumps(out), flush=True)
     if ipc:
         ipc.close()
@@ -819,6 +820,32 @@ def committed_legs():
 # LDS: SQ_LDS_IDX_ACTIVE = LDS-array cycles over the 256 CUs' LDS.
 VALU_CYCLES_PER_INST = 4.0
 HASH_WALK_FLOOR_MS_PER_1E8 = 0.47  # XXH3-128 of 16-B keys + 7 exact positions, full occupancy (tools/mb_hash.hip)
+
+
+def native_record():
+    """What ran: the HIP library this process loaded (path, size, sha256 prefix),
+    the device it opened, the kernels' source sha, and the strategies the C2 /
+    C3 legs dispatched — so a bench line can be tied to native code."""
+    import hashlib
+
+    import lsmbloom
+    rec = {"library": os.path.relpath(lsmbloom.LIB_PATH, ROOT), "kernel_sources_sha": build_sources_sha()}
+    try:
+        with open(lsmbloom.LIB_PATH, "rb") as f:
+            blob = f.read()
+        rec["library_bytes"] = len(blob)
+        rec["library_sha256_16"] = hashlib.sha256(blob).hexdigest()[:16]
+    except OSError as e:
+        rec["library_error"] = repr(e)[:120]
+    try:
+        import torch
+        rec["device"] = torch.cuda.get_device_name(torch.cuda.current_device())
+        rec["gcn_arch"] = getattr(torch.cuda.get_device_properties(torch.cuda.current_device()), "gcnArchName", None)
+    except Exception as e:  # never lose the bench line
+        rec["device_error"] = repr(e)[:120]
+    rec["abi_version"] = int(lsmbloom.lib().lsmb_abi_version())
+    rec["c2_build_strategy"] = lsmbloom.build_strategy(956715292, 100_000_000)
+    return rec
 
 
 def leg_roofline(leg, alg_bytes, kernel_ms, kernel, legs=None):
