@@ -840,6 +840,11 @@ void launch_hash_var(const VarLen& src, uint64_t n, Out out, hipStream_t st) {
     k_hash_var<0, LSMB_HV_KEYS, LSMB_HV_WIN, LSMB_HV_WPE, Out><<<dim3((uint32_t)g), dim3(LSMB_HV_KEYS), 0, st>>>(src.d, src.o, n, out);
 }
 
+template <class W>
+struct WalkTag {  // a walk type as a value (dispatch lambdas)
+    using type = W;
+};
+
 template <class Src>
 hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k, uint32_t* gw,
                       BuildStrategy s, const PartitionWorkspace& ws, int num_cus, hipStream_t st,
@@ -971,21 +976,26 @@ hipError_t build_with(const Src& src, uint64_t n, uint32_t num_bits, uint32_t k,
             auto go7 = [&](auto slc) {  // k = 7 (BloomFilter::new at fpr 0.01), bin width 2^SL
                 constexpr int SL = decltype(slc)::value;
                 const bool two = pl.keys_per_lane == 2;
-                if (list) {
-                    if (w32 && full) go(k_bin<Src, Walk32, 7, true, true, 1, SL, true>);
-                    else if (w32) go(k_bin<Src, Walk32, 7, true, false, 1, SL, true>);
-                    else if (full) go(k_bin<Src, Walk64, 7, true, true, 1, SL, true>);
-                    else go(k_bin<Src, Walk64, 7, true, false, 1, SL, true>);
-                } else if (w32) {
-                    if (full && two) go(k_bin<Src, Walk32, 7, true, true, 2, SL>);
-                    else if (full) go(k_bin<Src, Walk32, 7, true, true, 1, SL>);
-                    else if (two) go(k_bin<Src, Walk32, 7, true, false, 2, SL>);
-                    else go(k_bin<Src, Walk32, 7, true, false, 1, SL>);
+                auto pick = [&](auto wtag) {
+                    using W = typename decltype(wtag)::type;
+                    if (list) {
+                        if (full) go(k_bin<Src, W, 7, true, true, 1, SL, true>);
+                        else go(k_bin<Src, W, 7, true, false, 1, SL, true>);
+                    } else {
+                        if (full && two) go(k_bin<Src, W, 7, true, true, 2, SL>);
+                        else if (full) go(k_bin<Src, W, 7, true, true, 1, SL>);
+                        else if (two) go(k_bin<Src, W, 7, true, false, 2, SL>);
+                        else go(k_bin<Src, W, 7, true, false, 1, SL>);
+                    }
+                };
+                if (w32) {
+                    pick(WalkTag<Walk32>{});
+                } else if constexpr (!kRec) {
+                    // the saturated u32 filter (C5): folds instead of reductions
+                    if (num_bits == kMersenneBits) pick(WalkTag<WalkM>{});
+                    else pick(WalkTag<Walk64>{});
                 } else {
-                    if (full && two) go(k_bin<Src, Walk64, 7, true, true, 2, SL>);
-                    else if (full) go(k_bin<Src, Walk64, 7, true, true, 1, SL>);
-                    else if (two) go(k_bin<Src, Walk64, 7, true, false, 2, SL>);
-                    else go(k_bin<Src, Walk64, 7, true, false, 1, SL>);
+                    pick(WalkTag<Walk64>{});
                 }
             };
             if (k == 7) {

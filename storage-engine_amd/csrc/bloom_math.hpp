@@ -196,6 +196,39 @@ struct Walk64 {
 // The 64-bit-safe walk, used where d may exceed 2^31.
 using PosWalk = Walk64;
 
+// num_bits = 2^32 - 1: BloomFilter::new saturates `as u32` there
+// (src/bloom/mod.rs:49), so every filter sized for more than ~4.5e8 keys at
+// fpr 0.01 has it (C5's new(1e9, 0.01)).  2^32 = 1 (mod d): x mod d folds
+// the two halves (an add with end-around carry), and 2^64 mod d = 1, so no
+// reduction needs a quotient estimate.
+LSMB_HD uint32_t fold_m32(uint64_t x) {  // x mod (2^32 - 1)
+    uint32_t u;
+    const bool c = __builtin_add_overflow((uint32_t)x, (uint32_t)(x >> 32), &u);
+    u += c ? 1u : 0u;  // (<= 2^32 - 1 after a carry)
+    return u == 0xFFFFFFFFu ? 0u : u;
+}
+
+struct WalkM {  // d = 2^32 - 1 exactly; positions identical to Walk64's
+    using Mod = Mod32;
+    uint64_t x, h2;
+    uint32_t r, s0, s1;
+
+    LSMB_HD WalkM(const Mod32&, uint64_t h1, uint64_t h2_) : x(h1), h2(h2_) {
+        r = fold_m32(h1);
+        s0 = fold_m32(h2_);
+        s1 = s0 ? s0 - 1 : 0xFFFFFFFEu;  // (h2 - 2^64) mod d = s0 - 1
+    }
+    LSMB_HD WalkM(const Mod32& md, const H128& h) : WalkM(md, h.lo, h.hi) {}
+    LSMB_HD uint32_t pos() const { return r; }
+    LSMB_HD void next(const Mod32&) {
+        uint64_t nx;
+        const bool carry = __builtin_add_overflow(x, h2, &nx);
+        x = nx;
+        r = add_mod_wide(r, carry ? s1 : s0, 0xFFFFFFFFu);
+    }
+};
+constexpr uint32_t kMersenneBits = 0xFFFFFFFFu;  // the num_bits WalkM serves
+
 // A key's walk reduced to 12 bytes, for builds that hash in a separate kernel
 // (variable-length and odd-length keys): r = h1 mod d, s = h2 mod d and the
 // carries c_i of the wrapping sums h1 + i*h2 (bit i-1 = carry out of

@@ -5,7 +5,8 @@
 // x.  Mod32::reduce (any d < 2^32), Mod32::reduce31 (d <= 2^31, the 32-bit
 // remainder path Walk32 takes) and Mod14::reduce (d < 2^14).  Their biased-low
 // reciprocals (make) must keep every quotient estimate at floor(y/d) or one
-// below.  Host build of the device header (tests/test_capi_host.py).
+// below; and WalkM's positions for d = 2^32 - 1.  Host build of the device
+// header (tests/test_capi_host.py).
 #include <stdio.h>
 
 #include <random>
@@ -66,6 +67,28 @@ int main() {
         moduli(d, rng, 200);
     }
     for (uint32_t d = 1; d < (1u << 14); d++) moduli(d, rng, 40);  // every Mod14 modulus
+    // WalkM (d = 2^32 - 1): seven positions per (h1, h2) against a literal
+    // (h1 + i h2 mod 2^64) % d, random and edge hashes (0, d, 2^64 - 1, ...)
+    {
+        const uint32_t d = 0xFFFFFFFFu;
+        const Mod32 md = Mod32::make(d);
+        const uint64_t edge[] = {0, 1, d, (uint64_t)d + 1, 2ull * d, ~0ull, ~0ull - 1, 1ull << 63, (uint64_t)d << 32,
+                                 ((uint64_t)d << 32) + d};
+        auto walk = [&](uint64_t h1, uint64_t h2) {
+            WalkM w(md, h1, h2);
+            for (uint64_t i = 0; i < 7; i++) {
+                const uint64_t want = (h1 + i * h2) % d;
+                checked++;
+                if (w.pos() != want && bad++ < 20)
+                    printf("FAIL walkM h1=%llu h2=%llu i=%llu got=%u want=%llu\n", (unsigned long long)h1,
+                           (unsigned long long)h2, (unsigned long long)i, w.pos(), (unsigned long long)want);
+                w.next(md);
+            }
+        };
+        for (uint64_t a : edge)
+            for (uint64_t b : edge) walk(a, b);
+        for (int t = 0; t < 2000000; t++) walk(rng(), rng());
+    }
     printf("reduce: %ld checked, %ld bad\n", checked, bad);
     return bad ? 1 : 0;
 }

@@ -272,8 +272,8 @@ def test_reductions_at_quotient_edges(tmp_path):
     Mod14::reduce against a literal 64-bit % at the inputs that stress their
     biased-low quotient estimates: x = q*d + {0, 1, d-1} for extreme q, x near
     0 and 2^64, multiples of d, over fixed edge moduli (2^30, 2^31, 2^32-1 ...)
-    and random ones (tests/cpp/reduce_test.cpp, host build of the device
-    header)."""
+    and random ones; and WalkM, the fold walk of the saturated 2^32-1-bit
+    filter (tests/cpp/reduce_test.cpp, host build of the device header)."""
     import subprocess
     exe = str(tmp_path / "reduce_test")
     src = os.path.join(ROOT, "tests", "cpp", "reduce_test.cpp")
