@@ -1119,7 +1119,11 @@ PartitionPlan plan_partition_sl(uint32_t num_bits, uint32_t k, uint64_t n, int n
     if (k == 7) {
         const char* e = getenv("LSMB_SWEEP_PER");
         const uint32_t need2 = (kSegEntries + (uint32_t)ceil(2 * lambda + 2.0 * sqrt(2 * lambda)) + 7) & ~7u;
-        if ((pl.sweeps > 1 && pl.ring + 8 >= need2 && !(e && atoi(e) == 1)) || (e && atoi(e) == 2)) pl.keys_per_lane = 2;
+        // Not for the saturated 2^32-1-bit filter: with its fold walk (WalkM)
+        // the doubled phase is slower (C5 shard, accumulate: pass A 2.074 ->
+        // 2.136 ms; tools/r04_c5per.sh).
+        const bool auto2 = pl.sweeps > 1 && pl.ring + 8 >= need2 && num_bits != kMersenneBits;
+        if ((auto2 && !(e && atoi(e) == 1)) || (e && atoi(e) == 2)) pl.keys_per_lane = 2;
     }
     // 1024-thread workgroups (one resident per CU), at least ~kBinBlock keys
     // each: two per CU for 2^20-bit bins — pass B then streams twice as many,
