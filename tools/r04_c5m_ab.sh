@@ -1,7 +1,7 @@
 #!/bin/bash
 # C5 shard A/B on one box (125 M keys into new(1e9, 0.01) = 2^32-1 bits, fresh
-# sweeps): lib/liblsmbloom_prev.so (Walk64: quotient-estimate reductions) vs
-# this tree (WalkM: the saturated filter's positions by folding), two reps.
+# sweeps): lib/liblsmbloom_prev.so (the committed kernels) vs
+# this tree (r04m: WalkM; r04ab: branch-free half select in k_apply<21>), two reps.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 TAG=${1:-r04m}
 mkdir -p gpurun_out/$TAG
