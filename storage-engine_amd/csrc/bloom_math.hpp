@@ -243,6 +243,9 @@ struct WalkRec {
         if (md.d <= 0x80000000u) {  // (uniform) the 32-bit remainder path, as Walk32 takes
             q.r = md.reduce31(h.lo);
             q.s = md.reduce31(h.hi);
+        } else if (md.d == 0xFFFFFFFFu) {  // the saturated filter: folds (WalkM)
+            q.r = fold_m32(h.lo);
+            q.s = fold_m32(h.hi);
         } else {
             q.r = md.reduce(h.lo);
             q.s = md.reduce(h.hi);

@@ -248,6 +248,21 @@ def test_build_var_partial_last_block(ctx, oracle, tail):
     _cmp(ctx.build_var(blob, offs, nb, k), oracle.build_var(blob, offs, nb, k))
 
 
+def test_build_walk_records_saturated_filter(ctx, oracle):
+    """Var-len and odd-length keys into the saturated 2^32-1-bit filter
+    (new(1e9, 0.01)): the hash kernels write walk records whose remainders
+    are folds there (2^32 = 1 mod d), replayed by the 64-bit record walk in
+    two sweeps; every word vs the oracle."""
+    n = 3_000_000
+    nb, k = lsmbloom.params(10**9, 0.01)
+    assert nb == 2**32 - 1
+    data, offs = keygen.varlen(n)
+    assert lsmbloom.build_strategy(nb, n, k) == "partition" and lsmbloom.build_sweeps(nb, n, k) == 2
+    _cmp(ctx.build_var(data, offs, nb, k), oracle.build_var_mt(data, offs, nb, k, 16))
+    keys7 = np.ascontiguousarray(keygen.key16(0x5A7, 0, n)[:, :7])
+    _cmp(ctx.build_fixed(keys7, 7, nb, k), oracle.build_fixed_mt(keys7, 7, nb, k, 16))
+
+
 def test_build_var_c4_shape(ctx, oracle):
     n = 1_000_000
     data, offs = keygen.varlen(n)
