@@ -38,7 +38,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=20)  # ~28 ms of C2 steps: the clock has ramped (tools/r04_warm.sh)
+    ap.add_argument("--warmup", type=int, default=20)  # ~28 ms of C2 steps: the clock has ramped (tools/archive/r04_warm.sh)
     ap.add_argument("--global-keys", type=int, default=0,
                     help="keys of the whole run, split over the ranks (default: 1e8 = C2 at N=1, 1e9 = C5 at N>1)")
     ap.add_argument("--keys-per-gpu", type=int, default=0,
