@@ -143,6 +143,7 @@ def test_build_partition_huge_filter(ctx, oracle):
     (24_000_000, 200_000_000, 0.01, False, 1),   # 1825 2^20-bit slices -> one sweep of 2^21-bit bins
     (20_000_000, 10**9, 0.01, False, 2),         # C5's filter: 2 sweeps of 2^21-bit bins
     (20_000_000, 10**9, 0.01, True, 4),          # the same with 2^20-bit bins pinned: 4 sweeps
+    (20_000_000, 200_000_000, 0.01, True, 2),    # a Walk32 filter (< 2^31 bits) in 2 sweeps of 2^20-bit bins
     (6_000_000, 10**9, 0.001, False, 4),         # k = 10: generic-k kernels keep 2^20-bit bins
 ])
 def test_build_multi_sweep_steady_state(ctx, oracle, monkeypatch, n, filter_keys, fpr, slice20, sweeps):
