@@ -283,3 +283,23 @@ def test_reductions_at_quotient_edges(tmp_path):
     out = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
     assert ", 0 bad" in out.stdout
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    """No HIP library, no product: the mirror raises instead of falling back
+    to the oracle or any host path (fresh interpreter, library path pointed
+    at a file that does not exist)."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import lsmbloom\n"
+            "try:\n"
+            "    lsmbloom.lib()\n"
+            "except ImportError as e:\n"
+            "    print('raised:', e)\n"
+            "    sys.exit(3)\n"
+            "sys.exit(0)\n") % os.path.join(ROOT, "storage-engine_amd")
+    env = dict(os.environ, LSMB_LIB=str(tmp_path / "liblsmbloom_missing.so"))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 3, (r.returncode, r.stdout, r.stderr)
+    assert "not built" in r.stdout
