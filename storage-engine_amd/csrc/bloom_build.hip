@@ -655,7 +655,7 @@ __global__ __launch_bounds__(256) void k_ovf_apply(const uint32_t* __restrict__ 
 //      one lane-parallel load up front (lane j: region v + 16 j), then each
 //      region's 16-B pieces are loaded U per lane at a time and every 20-bit
 //      offset is ORed into LDS;
-//   3. the slice is written back once.
+//   3. the slice is written back once, with non-temporal stores.
 // fresh (BloomFilter::new + inserts, LIST pass A): the slice starts from zero
 // instead of its words in HBM, which are then write-only; a unit marked in
 // `dirty` ORs in (and clears) its overflow words.
@@ -754,7 +754,16 @@ __global__ __launch_bounds__(kApplyBlock) void k_apply(const uint64_t* __restric
             }
         }
         __syncthreads();
-        for (uint32_t i = tid; i < nw2; i += kApplyBlock) g2[i] = f2[i];
+        // Non-temporal write-back (one global_store_dwordx2 ... nt per word
+        // pair): this build reads the words no more, and dirty lines left in
+        // L2 / MALL were written back during the next build's pass A instead
+        // (C2 pass A 1.003 -> 0.979 ms, step 1.389 -> 1.371 ms;
+        // profiles/r04/r04ntw_writeback_ab.log).
+        for (uint32_t i = tid; i < nw2; i += kApplyBlock) {
+            const uint2 v = f2[i];
+            __builtin_nontemporal_store(v.x, &g2[i].x);
+            __builtin_nontemporal_store(v.y, &g2[i].y);
+        }
         if (dty && tid == 0) dirty[unit] = 0u;  // every thread read it before the first barrier
         __syncthreads();
     }
