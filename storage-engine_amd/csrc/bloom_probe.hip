@@ -58,6 +58,10 @@ struct SlicedFilters {
     uint32_t ob[32];        // filter f's output bit
 };
 
+// Answer rows are stored with the non-temporal policy: nothing in the call
+// reads them, and they then leave L2 / MALL to the keys (C3 probe 0.0432 ->
+// 0.0425 ms, filter sets -1 %; profiles/r04/r04outnt_probe_rows_ab.log).
+
 // Grid-wide rounds over n items for the 1024-thread C3 probe: round j is
 // items [j*gs, (j+1)*gs), lane L of the grid takes item j*gs + L.  Each
 // round's keys and rows are addressed through a buffer resource whose base
@@ -198,7 +202,7 @@ __global__ __launch_bounds__(BS) void k_probe_sliced(Src src, uint64_t n, typena
                 m &= table[pw.pos()];
                 if (jj + 1 < K) pw.next(md);
             }
-            __builtin_amdgcn_raw_buffer_store_b8(m, R.rsrc(out, j, 1), R.lane, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b8(m, R.rsrc(out, j, 1), R.lane, 0, 2 /* nt */);
         };
         for (uint32_t j = 0; j < R.rounds; j += 3) {  // past the last round: empty windows (zeros, dropped rows)
             row(ka, j);
@@ -521,7 +525,7 @@ __global__ __launch_bounds__(BS) void k_fset_sliced(Src src, uint64_t n, const R
             for (uint32_t f = 0; f < nfilt; f++)
                 if ((m >> f) & 1) o |= 1ull << fl[f].f.out_bit;
         }
-        out[i] = o;
+        __builtin_nontemporal_store(o, &out[i]);  // (non-temporal rows: tools/archive/r04_out_nt.sh)
     }
 }
 
@@ -681,7 +685,7 @@ __global__ __launch_bounds__(kClassBlock, 4 * class_wgs_per_cu<Src>()) void k_fs
             }
             o = s;
         }
-        out[i] = o;
+        __builtin_nontemporal_store(o, &out[i]);  // (non-temporal rows: tools/archive/r04_out_nt.sh)
     }
 }
 
