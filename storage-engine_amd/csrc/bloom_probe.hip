@@ -157,7 +157,7 @@ __global__ __launch_bounds__(BS) void k_probe_sliced(Src src, uint64_t n, typena
     // loop of 32 x 8 bit extracts ran on 299 threads: ~900 VALU each).
     bool ident = sizeof(T) == 1;
 #pragma unroll
-    for (uint32_t f = 0; f < FMAX; f++) ident = ident && ob[f] == f;
+    for (uint32_t f = 0; f < FMAX; f++) ident = ident && (f >= nfilt || ob[f] == f);  // absent slots: vm[f] = 0
     if (ident) {
         for (uint32_t it = threadIdx.x; it < 4 * nw32; it += blockDim.x) {
             const uint32_t w = it >> 2, sh = 8 * (it & 3);
@@ -726,20 +726,21 @@ hipError_t fset_probe_with(const Src& src, uint64_t n, const RangedFilter* df, u
                 if (bs != 1024)  // (the 1024-thread kernels' table is static LDS)
                     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
                 const uint64_t gb = bs == 256 ? g : std::min<uint64_t>((n + bs - 1) / bs, probe_wgs_per_cu(2) * num_cus);
-                launch_done(kern, dim3((uint32_t)std::max<uint64_t>(gb, 1)), dim3(bs), bs == 1024 ? 0u : (uint32_t)smem, st,
-                            done, src, n, df, nfilt, rg, shared_k, md, out);
+                return launch_done(kern, dim3((uint32_t)std::max<uint64_t>(gb, 1)), dim3(bs),
+                                   bs == 1024 ? 0u : (uint32_t)smem, st, done, src, n, df, nfilt, rg, shared_k, md, out);
             };
+            // (launch_done has consumed any launch error: return its result)
             if (tsz == 1) {
                 if (shared_k == 7 && std::is_same<Src, Fixed16>::value && Mod14::fits(shared_nb))
-                    go(k_fset_sliced<Src, uint8_t, 7, 1024, Walk14>, Mod14::make(shared_nb), 1024);
-                else if (shared_k == 7 && std::is_same<Src, Fixed16>::value)
-                    go(k_fset_sliced<Src, uint8_t, 7, 1024>, m32, 1024);
-                else if (shared_k == 7) go(k_fset_sliced<Src, uint8_t, 7>, m32);
-                else go(k_fset_sliced<Src, uint8_t, 0>, m32);
-            } else if (tsz == 2) go(k_fset_sliced<Src, uint16_t, 0>, m32);
-            else if (tsz == 4) go(k_fset_sliced<Src, uint32_t, 0>, m32);
-            else go(k_fset_sliced<Src, uint64_t, 0>, m32);
-            return hipGetLastError();
+                    return go(k_fset_sliced<Src, uint8_t, 7, 1024, Walk14>, Mod14::make(shared_nb), 1024);
+                if (shared_k == 7 && std::is_same<Src, Fixed16>::value)
+                    return go(k_fset_sliced<Src, uint8_t, 7, 1024>, m32, 1024);
+                if (shared_k == 7) return go(k_fset_sliced<Src, uint8_t, 7>, m32);
+                return go(k_fset_sliced<Src, uint8_t, 0>, m32);
+            }
+            if (tsz == 2) return go(k_fset_sliced<Src, uint16_t, 0>, m32);
+            if (tsz == 4) return go(k_fset_sliced<Src, uint32_t, 0>, m32);
+            return go(k_fset_sliced<Src, uint64_t, 0>, m32);
         }
     }
     return launch_done(k_fset_probe<Src>, dim3((uint32_t)g), dim3(256), 0u, st, done, src, n, df, nfilt, rg, out);

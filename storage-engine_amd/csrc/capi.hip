@@ -170,10 +170,12 @@ int build_dev_ws(lsmb_ctx* c, const KeyBatch& kb_all, uint32_t num_bits, uint32_
         // of the whole filter for lists that fill up, zeroed once when
         // (re)allocated
         const uint64_t units = ((nwords64(num_bits) * 2) + kSliceWords32 - 1) / kSliceWords32;
+        // each buffer is zeroed right after it is (re)allocated, before the
+        // next allocation can fail: a grown buffer never stays unzeroed
         const size_t ob = c->ws_ovf.bytes, db = c->ws_dirty.bytes;
         HIP_TRY(c->ws_ovf.ensure(units * kSliceWords32 * 4));
-        HIP_TRY(c->ws_dirty.ensure(units * 4));
         if (c->ws_ovf.bytes != ob) HIP_TRY(hipMemsetAsync(c->ws_ovf.p, 0, c->ws_ovf.bytes, st));
+        HIP_TRY(c->ws_dirty.ensure(units * 4));
         if (c->ws_dirty.bytes != db) HIP_TRY(hipMemsetAsync(c->ws_dirty.p, 0, c->ws_dirty.bytes, st));
         ws.ovf = (uint32_t*)c->ws_ovf.p;
         ws.dirty = (uint32_t*)c->ws_dirty.p;

@@ -43,9 +43,10 @@ struct OrSources {
 
 // dst[i] = OR over j of src_j[i], i < count (elements of V).  dst may be one
 // of the sources (the owner's own partial): each element is read by every
-// source load before its one store, by the same thread.
+// source load before its one store, by the same thread.  So dst is not
+// __restrict__ (it aliases a source).
 template <class V>
-__global__ __launch_bounds__(256) void k_or_gather(V* __restrict__ dst, OrSources src, uint64_t count) {
+__global__ __launch_bounds__(256) void k_or_gather(V* dst, OrSources src, uint64_t count) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
         V v = static_cast<const V*>(src.p[0])[i];

@@ -132,8 +132,17 @@ class IpcMerge:
         words[lo:hi] is waited for first; returns when every rank's range is
         merged (host-synchronous)."""
         hi = self.words.numel() if hi is None else hi
+        if not 0 <= lo <= hi <= self.words.numel():
+            raise ValueError("word range [%d, %d) outside this rank's %d words" % (lo, hi, self.words.numel()))
         stream = stream or torch.cuda.current_stream(self.words.device)
-        self._phase_done(stream)  # every partial of the range is final
+        stream.synchronize()
+        # every partial of the range is final; the exchange that orders this
+        # phase also checks that every rank merges the same range (the peer
+        # loads use raw pointers into the other ranks' words)
+        rng = torch.tensor([lo, hi, -lo, -hi], dtype=torch.int64)
+        dist.all_reduce(rng, op=dist.ReduceOp.MAX, group=self.group)
+        if rng.tolist() != [lo, hi, -lo, -hi]:
+            raise ValueError("ranks disagree on the word range: this rank [%d, %d)" % (lo, hi))
         per = _slices(hi - lo, self.world)
         sl = [(min(hi, lo + r * per), min(hi, lo + (r + 1) * per)) for r in range(self.world)]
         a, b = sl[self.rank]

@@ -340,7 +340,7 @@ def _c3_filters(oracle, nfilt=8, members=1000):
     return fl, np.concatenate(mem)
 
 
-@pytest.mark.parametrize("nfilt", [1, 3, 8, 9, 16, 17, 32])
+@pytest.mark.parametrize("nfilt", [1, 3, 5, 7, 8, 9, 16, 17, 32])
 def test_probe_sliced_vs_oracle(ctx, oracle, nfilt):
     fl, mem = _c3_filters(oracle, nfilt)
     q = 200_000
