@@ -326,11 +326,10 @@ def main():
             allreduce()
             return
         main = torch.cuda.current_stream(dev)
-        if ipc:  # every sweep queued first: the host waits per range while the next sweep builds
-            for s in range(nsw):
+        if ipc:  # device-ordered: the merge is only enqueued, the host never waits inside it
+            for s, (a, b) in enumerate(ranges):
                 ctx.build_fixed_dev_sweep_new(keys, 16, npg, nb, k, words, s)
                 sweep_ev[s].record(main)
-            for s, (a, b) in enumerate(ranges):
                 side.wait_event(sweep_ev[s])
                 ipc.allreduce(a, b, stream=side)
             main.wait_stream(side)
@@ -449,7 +448,7 @@ def main():
         out["step_split"] = {"build_ms": round(build_ms, 4), "or_allreduce_ms": round(coll_ms, 4),
                              "what": "serial steps (untimed pass), slowest rank: device build (fresh) / "
                                      + ("bitwise-OR allreduce by peer loads over IPC-mapped words (OR gather "
-                                        "reduce-scatter + copy all-gather, host barriers between phases)"
+                                        "reduce-scatter + copy all-gather, phases ordered by device flags)"
                                         if ipc else
                                         "bitwise-OR allreduce (all_to_all reduce-scatter + native OR kernel "
                                         "+ all_gather)") + " of the whole filter",
@@ -458,6 +457,9 @@ def main():
                              "timed_step": ("%d build sweeps, each sweep's word range OR-allreduced on a side "
                                             "stream while the next sweep builds" % nsw) if overlap
                                            else "build then OR-allreduce",
+                             "merge": ("ipc (peer loads, device-ordered flags)" if ipc else
+                                       "rccl all_to_all + OR kernel + all_gather" if args.backend == "nccl" else
+                                       "%s collectives (host-staged) + OR kernel" % args.backend),
                              "or_allreduce_bytes_per_gpu": int(moved),
                              "or_allreduce_GBs_per_gpu": round(moved / (coll_ms * 1e-3) / 1e9, 1) if coll_ms else None}
         # Self-check (outside the timed region): one more sharded step; rank 0
@@ -488,6 +490,9 @@ def main():
                 del ref, buf
             except Exception as e:  # report, never lose the bench line
                 out["multi_gpu_check_error"] = repr(e)[:200]
+        if ipc:
+            torch.cuda.synchronize(dev)
+            out["step_split"]["flag_timeouts"] = int(max_over_ranks(ipc.timeouts()))
         dist.barrier()
 
     # Full-size parity in the bench line itself: the filter the timed steps built
@@ -604,7 +609,7 @@ def compact_line(out):
         ss = out["step_split"]
         c["step_split"] = {k: ss.get(k) for k in ("build_ms", "or_allreduce_ms", "serial_ms_per_step",
                                                   "or_allreduce_bytes_per_gpu", "or_allreduce_GBs_per_gpu",
-                                                  "overlap_calibration")}
+                                                  "overlap_calibration", "timed_step", "merge", "flag_timeouts")}
     if "single_gpu_same_workload" in out:
         sg = out["single_gpu_same_workload"]
         c["single_gpu_same_workload"] = {"ms": sg.get("ms"), "value": sg.get("value")}

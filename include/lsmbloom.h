@@ -351,6 +351,29 @@ int lsmb_ipc_close(lsmb_ctx* ctx, void* d_base);
 int lsmb_or_gather_dev(lsmb_ctx* ctx, void* d_dst, const void* const* d_srcs, uint32_t nsrc, uint64_t nwords,
                        void* stream);
 
+/* Device-ordered phases for the merge above, so that no host waits inside it:
+ * a flag is a u32 epoch counter in device memory (this process's own, or a
+ * peer's mapped with lsmb_ipc_import).  The merge of epoch e on `stream` is
+ *   signal(own flag[0], e); wait(every rank's flag[0] >= e)   partials final
+ *   or_gather (reduce-scatter);  signal(flag[1], e); wait(all flag[1] >= e)
+ *   or_gather copies (all-gather); signal(flag[2], e); wait(all flag[2] >= e)
+ * (lsmbloom.dist.IpcMerge).  All enqueue and return at once. */
+
+/* After everything before it on `stream`: a system-scope release store of
+ * `value` into *d_flag. */
+int lsmb_flag_signal_dev(lsmb_ctx* ctx, uint32_t* d_flag, uint32_t value, void* stream);
+
+/* Later work on `stream` waits until every d_flags[j] >= value (epoch compare,
+ * wrap-safe), j < nflags <= 64.  A flag still short after timeout_ms counts
+ * one timeout (lsmb_flag_timeouts) and the wait ends anyway: a dead peer can
+ * never hang the queue. */
+int lsmb_flag_wait_dev(lsmb_ctx* ctx, const uint32_t* const* d_flags, uint32_t nflags, uint32_t value,
+                       uint32_t timeout_ms, void* stream);
+
+/* Waits of this context that timed out so far (a synchronous read: call it
+ * after the streams that waited have finished). */
+int lsmb_flag_timeouts(lsmb_ctx* ctx, uint32_t* count);
+
 /* ---- device-resident filter sets (multi-get pre-check) --------------------- */
 /* An lsmb_fset keeps up to 64 SSTable filters resident in device memory, each
  * with its table's key range [min_key, max_key] (SSTable meta,

@@ -62,6 +62,43 @@ __global__ __launch_bounds__(256) void k_or_gather(V* dst, OrSources src, uint64
     }
 }
 
+// ---- device-ordered phase flags (cross-process merge, lsmb_flag_*) --------
+// A flag is a u32 epoch counter in device memory (this process's, or a peer's
+// mapped over IPC).  signal: one system-scope release store of the epoch after
+// everything before it on the stream (kernel boundaries already release each
+// kernel's stores at agent scope, i.e. L2 written back across the XCDs).
+// wait: one wave, lane j polls flag j with system-scope loads (no stale L2
+// copy) until it reaches the epoch (wrap-safe compare), backing off with
+// s_sleep; every lane gives up after `ticks` of the constant-rate wall clock
+// and counts a timeout instead, so the kernel always ends (a peer that died
+// cannot hang the queue).
+constexpr uint32_t kMaxFlags = 64;
+struct FlagSet {
+    const uint32_t* p[kMaxFlags];
+    uint32_t n;
+};
+
+__global__ __launch_bounds__(64) void k_flag_signal(uint32_t* flag, uint32_t value) {
+    if (threadIdx.x == 0) __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(64) void k_flag_wait(FlagSet fs, uint32_t value, uint64_t ticks, uint32_t* timeouts) {
+    const uint32_t j = threadIdx.x;
+    if (j < fs.n) {
+        const uint64_t t0 = (uint64_t)wall_clock64();
+        for (;;) {
+            const uint32_t v = __hip_atomic_load(fs.p[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if ((int32_t)(v - value) >= 0) break;
+            if ((uint64_t)wall_clock64() - t0 > ticks) {
+                atomicAdd(timeouts, 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(8);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: later reads see the peers' data
+}
+
 hipError_t launch_or_gather(uint64_t* dst, const OrSources& s, uint64_t nwords, int num_cus, hipStream_t st) {
     if (nwords == 0) return hipSuccess;
     bool a16 = ((uintptr_t)dst & 15) == 0 && (nwords & 1) == 0;
@@ -438,6 +475,52 @@ int lsmb_or_gather_dev(lsmb_ctx* c, void* d_dst, const void* const* d_srcs, uint
     if (((uintptr_t)d_dst & 7) != 0) return fail(LSMB_EINVAL, "d_dst is not 8-byte aligned");
     DevGuard g(c->dev);
     HIP_TRY(launch_or_gather((uint64_t*)d_dst, s, nwords, c->num_cus, pick_stream(c, stream)));
+    return LSMB_OK;
+}
+
+int lsmb_flag_signal_dev(lsmb_ctx* c, uint32_t* d_flag, uint32_t value, void* stream) {
+    if (!c || !d_flag) return fail(LSMB_EINVAL, "null argument");
+    if (((uintptr_t)d_flag & 3) != 0) return fail(LSMB_EINVAL, "d_flag is not 4-byte aligned");
+    DevGuard g(c->dev);
+    k_flag_signal<<<dim3(1), dim3(64), 0, pick_stream(c, stream)>>>(d_flag, value);
+    HIP_TRY(hipGetLastError());
+    return LSMB_OK;
+}
+
+int lsmb_flag_wait_dev(lsmb_ctx* c, const uint32_t* const* d_flags, uint32_t nflags, uint32_t value,
+                       uint32_t timeout_ms, void* stream) {
+    if (!c || !d_flags) return fail(LSMB_EINVAL, "null argument");
+    if (nflags > kMaxFlags) return fail(LSMB_EINVAL, "nflags must be at most %u", kMaxFlags);
+    if (nflags == 0) return LSMB_OK;
+    FlagSet fs;
+    fs.n = nflags;
+    for (uint32_t j = 0; j < nflags; j++) {
+        if (!d_flags[j] || ((uintptr_t)d_flags[j] & 3) != 0) return fail(LSMB_EINVAL, "flag %u: null or unaligned", j);
+        fs.p[j] = d_flags[j];
+    }
+    DevGuard g(c->dev);
+    hipStream_t st = pick_stream(c, stream);
+    if (!c->flag_timeouts.p) {
+        HIP_TRY(c->flag_timeouts.ensure(64));
+        HIP_TRY(hipMemsetAsync(c->flag_timeouts.p, 0, 64, st));  // once per context, before the first wait
+    }
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->dev) != hipSuccess || khz <= 0) khz = 100000;
+    const uint64_t ticks = (uint64_t)timeout_ms * (uint64_t)khz;
+    k_flag_wait<<<dim3(1), dim3(64), 0, st>>>(fs, value, ticks, (uint32_t*)c->flag_timeouts.p);
+    HIP_TRY(hipGetLastError());
+    return LSMB_OK;
+}
+
+int lsmb_flag_timeouts(lsmb_ctx* c, uint32_t* count) {
+    if (!c || !count) return fail(LSMB_EINVAL, "null argument");
+    *count = 0;
+    if (!c->flag_timeouts.p) return LSMB_OK;
+    DevGuard g(c->dev);
+    // (the caller has finished the streams that waited; c->st orders this read
+    // after the zeroing when both ran on it)
+    HIP_TRY(hipMemcpyAsync(count, c->flag_timeouts.p, 4, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
     return LSMB_OK;
 }
 

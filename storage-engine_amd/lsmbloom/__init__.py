@@ -111,6 +111,10 @@ SIGNATURES = {
     "lsmb_ipc_import": (ctypes.c_int, [vp, u8p, ctypes.POINTER(vp)]),
     "lsmb_ipc_close": (ctypes.c_int, [vp, vp]),
     "lsmb_or_gather_dev": (ctypes.c_int, [vp, vp, ctypes.POINTER(vp), ctypes.c_uint32, ctypes.c_uint64, vp]),
+    "lsmb_flag_signal_dev": (ctypes.c_int, [vp, vp, ctypes.c_uint32, vp]),
+    "lsmb_flag_wait_dev": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                          vp]),
+    "lsmb_flag_timeouts": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint32)]),
     "lsmb_stream_open": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(vp)]),
     "lsmb_stream_reset": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32]),
     "lsmb_stream_close": (None, [vp]),
@@ -383,6 +387,23 @@ class Context:
         arr = (vp * len(src_ptrs))(*[vp(int(p)) for p in src_ptrs])
         _check(lib().lsmb_or_gather_dev(self.h, vp(int(dst_ptr)), arr, len(src_ptrs), int(nwords),
                                         self._stream(stream)))
+
+    def flag_signal_dev(self, flag_ptr, value, stream=None):
+        """After the stream's prior work: *flag = value, system-scope release (lsmb_flag_signal_dev)."""
+        _check(lib().lsmb_flag_signal_dev(self.h, vp(int(flag_ptr)), int(value) & 0xFFFFFFFF, vp(stream or 0)))
+
+    def flag_wait_dev(self, flag_ptrs, value, timeout_ms=20000, stream=None):
+        """Later work on the stream waits until every flag >= value, or timeout_ms
+        (then counted in flag_timeouts()) (lsmb_flag_wait_dev)."""
+        arr = (vp * len(flag_ptrs))(*[vp(int(p)) for p in flag_ptrs])
+        _check(lib().lsmb_flag_wait_dev(self.h, arr, len(flag_ptrs), int(value) & 0xFFFFFFFF, int(timeout_ms),
+                                        vp(stream or 0)))
+
+    def flag_timeouts(self):
+        """Flag waits of this context that timed out so far (lsmb_flag_timeouts)."""
+        n = ctypes.c_uint32(0)
+        _check(lib().lsmb_flag_timeouts(self.h, ctypes.byref(n)))
+        return int(n.value)
 
     def ipc_import(self, handle):
         """Maps another process's device allocation (lsmb_ipc_import) -> base pointer (int)."""

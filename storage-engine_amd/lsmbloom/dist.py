@@ -92,67 +92,148 @@ class IpcMerge:
       1. reduce-scatter: rank g ORs word-slice g of all G partials into its own
          words (one lsmb_or_gather_dev, G sources);
       2. all-gather: rank g copies every other merged slice from its owner.
-    `group` (gloo) only orders the phases: a host barrier after each rank's
-    stream finished the previous phase, and one at the end so that no rank
-    rewrites its words while a peer may still read them.  Per GPU it reads
-    (G-1)/G of the range twice over the peer links, the RCCL path's bytes."""
+    Per GPU it reads (G-1)/G of the range twice over the peer links, the RCCL
+    path's bytes.
 
-    def __init__(self, words, ctx, group=None):
+    Ordering (ordered="device", the default): the phases are ordered on the
+    GPUs, never on the host.  Every rank also exports a 3-word flag array; merge
+    number e enqueues on the caller's stream
+        signal(my flag[0] = e); wait(every rank's flag[0] >= e)   partials final
+        reduce-scatter;  signal(flag[1] = e); wait(all flag[1] >= e)
+        all-gather;      signal(flag[2] = e); wait(all flag[2] >= e)
+    (lsmb_flag_signal_dev / lsmb_flag_wait_dev) and returns at once: the host
+    never synchronises inside a merge, so a sweep's merge overlaps the next
+    sweep's build.  The last wait keeps any later work on the stream from
+    rewriting my words while a peer may still read them.  A wait that times
+    out (a dead peer) is counted, not hung on: close() / timeouts() report it.
+    `merge_schedule` below is the protocol as data (tests/test_ipc_protocol.py
+    runs it against simulated ranks).  ordered="host" is the round-4 form: a
+    stream synchronise plus a `group` barrier between phases.
+
+    `group` (gloo) exchanges the handles once, checks each new word range once
+    against every rank's, and orders close()."""
+
+    def __init__(self, words, ctx, group=None, ordered="device", timeout_ms=20000):
         import lsmbloom
-        self.words, self.ctx, self.group = words, ctx, group
+        if ordered not in ("device", "host"):
+            raise ValueError("ordered must be 'device' or 'host'")
+        self.words, self.ctx, self.group, self.ordered = words, ctx, group, ordered
+        self.timeout_ms = int(timeout_ms)
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        self.epoch = 0
+        self._checked = set()
+        # phase flags (epochs), zero before any peer can poll them: the handle
+        # exchange below happens after this synchronise
+        self.flags = torch.zeros(4, dtype=torch.int32, device=words.device)
+        torch.cuda.synchronize(words.device)
         h, off = lsmbloom.ipc_export(words)
+        fh, foff = lsmbloom.ipc_export(self.flags)
         allh = [None] * self.world
-        dist.all_gather_object(allh, (h, off, words.numel(), words.device.index), group=group)
-        self.bases, self.ptrs = [], []
-        for r, (hh, oo, n, _) in enumerate(allh):
+        dist.all_gather_object(allh, (h, off, words.numel(), fh, foff), group=group)
+        self.bases, self.ptrs, self.fptrs = [], [], []
+        for r, (hh, oo, n, fhh, foo) in enumerate(allh):
             if n != words.numel():
                 raise ValueError("rank %d's words hold %d words, mine %d" % (r, n, words.numel()))
             if r == self.rank:
                 self.ptrs.append(words.data_ptr())
+                self.fptrs.append(self.flags.data_ptr())
+                continue
+            base = ctx.ipc_import(hh)
+            self.bases.append(base)
+            self.ptrs.append(base + oo)
+            if fhh == hh:  # the flags share the words' allocation: one mapping
+                self.fptrs.append(base + foo)
             else:
-                base = ctx.ipc_import(hh)
-                self.bases.append(base)
-                self.ptrs.append(base + oo)
+                fbase = ctx.ipc_import(fhh)
+                self.bases.append(fbase)
+                self.fptrs.append(fbase + foo)
+
+    def timeouts(self):
+        """Flag waits that timed out so far on this rank (the caller has
+        finished the merging streams)."""
+        return self.ctx.flag_timeouts()
 
     def close(self):
+        torch.cuda.synchronize(self.words.device)
         dist.barrier(group=self.group)  # no peer reads my words any more
+        n = self.ctx.flag_timeouts()
         for b in self.bases:
             self.ctx.ipc_close(b)
-        self.bases, self.ptrs = [], []
+        self.bases, self.ptrs, self.fptrs = [], [], []
+        if n:
+            raise RuntimeError("IpcMerge: %d phase waits timed out (a peer never signalled)" % n)
 
     def _phase_done(self, stream):
         stream.synchronize()
         dist.barrier(group=self.group)
 
-    def allreduce(self, lo=0, hi=None, stream=None):
-        """In-place OR-allreduce of words[lo:hi] (word indices) over the group.
-        The caller's pending work on `stream` (default: current) that writes
-        words[lo:hi] is waited for first; returns when every rank's range is
-        merged (host-synchronous)."""
-        hi = self.words.numel() if hi is None else hi
-        if not 0 <= lo <= hi <= self.words.numel():
-            raise ValueError("word range [%d, %d) outside this rank's %d words" % (lo, hi, self.words.numel()))
-        stream = stream or torch.cuda.current_stream(self.words.device)
-        stream.synchronize()
-        # every partial of the range is final; the exchange that orders this
-        # phase also checks that every rank merges the same range (the peer
-        # loads use raw pointers into the other ranks' words)
+    def _check_range(self, lo, hi):
+        """The peer loads use raw pointers into the other ranks' words: every
+        rank must merge the same range.  Checked once per distinct range (the
+        ranks see the same sequence of ranges, so they agree on which are new)."""
+        if (lo, hi) in self._checked:
+            return
         rng = torch.tensor([lo, hi, -lo, -hi], dtype=torch.int64)
         dist.all_reduce(rng, op=dist.ReduceOp.MAX, group=self.group)
         if rng.tolist() != [lo, hi, -lo, -hi]:
             raise ValueError("ranks disagree on the word range: this rank [%d, %d)" % (lo, hi))
-        per = _slices(hi - lo, self.world)
-        sl = [(min(hi, lo + r * per), min(hi, lo + (r + 1) * per)) for r in range(self.world)]
-        a, b = sl[self.rank]
-        if b > a:
-            self.ctx.or_gather_dev(self.ptrs[self.rank] + 8 * a, [p + 8 * a for p in self.ptrs], b - a,
-                                   stream=stream.cuda_stream)
-        self._phase_done(stream)  # every slice merged
-        for r, (a, b) in enumerate(sl):
-            if r != self.rank and b > a:
-                self.ctx.or_gather_dev(self.ptrs[self.rank] + 8 * a, [self.ptrs[r] + 8 * a], b - a,
+        self._checked.add((lo, hi))
+
+    def allreduce(self, lo=0, hi=None, stream=None):
+        """In-place OR-allreduce of words[lo:hi] (word indices) over the group,
+        after the caller's pending work on `stream` (default: current).
+        ordered="device": enqueued only (returns at once); the stream's later
+        work sees the merged range.  ordered="host": returns when every rank's
+        range is merged."""
+        hi = self.words.numel() if hi is None else hi
+        if not 0 <= lo <= hi <= self.words.numel():
+            raise ValueError("word range [%d, %d) outside this rank's %d words" % (lo, hi, self.words.numel()))
+        self._check_range(lo, hi)
+        stream = stream or torch.cuda.current_stream(self.words.device)
+        if self.ordered == "host":
+            self._phase_done(stream)  # every partial of the range is final
+            for op in merge_schedule(self.rank, self.world, lo, hi, 0):
+                if op[0] == "gather":
+                    self._gather(op, stream)
+                elif op[0] == "wait" and op[1] in (1, 2):
+                    self._phase_done(stream)
+            return self.words
+        self.epoch += 1
+        for op in merge_schedule(self.rank, self.world, lo, hi, self.epoch):
+            if op[0] == "signal":
+                _, ph, e = op
+                self.ctx.flag_signal_dev(self.fptrs[self.rank] + 4 * ph, e, stream=stream.cuda_stream)
+            elif op[0] == "wait":
+                _, ph, e = op
+                self.ctx.flag_wait_dev([p + 4 * ph for p in self.fptrs], e, self.timeout_ms,
                                        stream=stream.cuda_stream)
-        self._phase_done(stream)  # every rank holds the merged range; words may be rewritten
+            else:
+                self._gather(op, stream)
         return self.words
+
+    def _gather(self, op, stream):
+        _, a, b, srcs = op
+        self.ctx.or_gather_dev(self.ptrs[self.rank] + 8 * a, [self.ptrs[r] + 8 * a for r in srcs], b - a,
+                               stream=stream.cuda_stream)
+
+
+def merge_schedule(rank, world, lo, hi, epoch):
+    """The device-ordered merge of words[lo:hi] as this rank's stream sees it,
+    in order: ("signal", phase, epoch) — set my flag[phase] = epoch;
+    ("wait", phase, epoch) — until every rank's flag[phase] >= epoch;
+    ("gather", a, b, ranks) — my words[a:b] = OR of those ranks' words[a:b]
+    (my own index among them: in place).  Phase 0: every partial of the range
+    is final; 1: every slice merged; 2: every rank holds the merged range."""
+    per = _slices(hi - lo, world)
+    sl = [(min(hi, lo + r * per), min(hi, lo + (r + 1) * per)) for r in range(world)]
+    ops = [("signal", 0, epoch), ("wait", 0, epoch)]
+    a, b = sl[rank]
+    if b > a:
+        ops.append(("gather", a, b, list(range(world))))
+    ops += [("signal", 1, epoch), ("wait", 1, epoch)]
+    for r, (a, b) in enumerate(sl):
+        if r != rank and b > a:
+            ops.append(("gather", a, b, [r]))
+    ops += [("signal", 2, epoch), ("wait", 2, epoch)]
+    return ops

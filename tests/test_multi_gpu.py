@@ -253,10 +253,12 @@ def test_dist_or_allreduce_device_path(oracle, world, n, filter_n):
         assert mine == _digest(sl), "rank %d reduce-scatter slice differs" % rank
 
 
-def _ipc_worker(rank, world, port, n, filter_n, per_sweep, q):
+def _ipc_worker(rank, world, port, n, filter_n, per_sweep, q, ordered="device", seeds=(0x5EED0001,)):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     sys.path.insert(0, os.path.join(ROOT, "storage-engine_amd"))
     sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import time
+
     import torch
     import torch.distributed as dist
 
@@ -269,21 +271,43 @@ def _ipc_worker(rank, world, port, n, filter_n, per_sweep, q):
         nb, k = lsmbloom.params(filter_n, 0.01)
         lo, hi = n * rank // world, n * (rank + 1) // world
         keys = torch.empty((hi - lo, 16), dtype=torch.uint8, device=dev)
-        ctx.gen_key16_dev(0x5EED0001, lo, hi - lo, keys)
         words = torch.empty(lsmbloom.num_words(nb), dtype=torch.int64, device=dev)
         words.fill_(-1)  # garbage: the fresh build writes every word
-        m = ldist.IpcMerge(words, ctx)
+        m = ldist.IpcMerge(words, ctx, ordered=ordered)
         nsw = lsmbloom.build_sweeps(nb, hi - lo, k)
-        if per_sweep:  # the bench's overlapped form: sweep s's range merged after sweep s
-            for s in range(nsw):
-                ctx.build_fixed_dev_sweep_new(keys, 16, hi - lo, nb, k, words, s)
-                a, b = lsmbloom.sweep_words(nb, hi - lo, s, k)
-                m.allreduce(a, b)
-        else:
-            ctx.build_fixed_dev_new(keys, 16, hi - lo, nb, k, words)
-            m.allreduce()
-        torch.cuda.synchronize()
-        q.put((rank, nsw, _digest(words.cpu().numpy().view(np.uint64))))
+        # host-side ordering inside a merge (device-ordered: none after the
+        # first, range-checking call of each range)
+        calls = {"sync": 0, "barrier": 0}
+        real_sync, real_barrier = torch.cuda.Stream.synchronize, dist.barrier
+
+        def count_sync(self):
+            calls["sync"] += 1
+            return real_sync(self)
+
+        def count_barrier(*a, **kw):
+            calls["barrier"] += 1
+            return real_barrier(*a, **kw)
+        digests = []
+        for i, seed in enumerate(seeds):
+            ctx.gen_key16_dev(seed, lo, hi - lo, keys)
+            torch.cuda.synchronize()
+            if rank == world - 1:
+                time.sleep(0.3)  # the last rank builds late: the others' merge must wait for it on the GPU
+            if i == 1:
+                torch.cuda.Stream.synchronize, dist.barrier = count_sync, count_barrier
+            if per_sweep:  # the bench's overlapped form: sweep s's range merged after sweep s
+                for s in range(nsw):
+                    ctx.build_fixed_dev_sweep_new(keys, 16, hi - lo, nb, k, words, s)
+                    a, b = lsmbloom.sweep_words(nb, hi - lo, s, k)
+                    m.allreduce(a, b)
+            else:
+                ctx.build_fixed_dev_new(keys, 16, hi - lo, nb, k, words)
+                m.allreduce()
+            torch.cuda.Stream.synchronize, dist.barrier = real_sync, real_barrier
+            torch.cuda.synchronize()
+            digests.append(_digest(words.cpu().numpy().view(np.uint64)))
+        timeouts = m.timeouts()
+        q.put((rank, nsw, digests, calls, timeouts))
         m.close()
         ctx.close()
     finally:
@@ -291,21 +315,30 @@ def _ipc_worker(rank, world, port, n, filter_n, per_sweep, q):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world,n,filter_n,per_sweep", [(2, 3_000_000, 30_000_000, False),
-                                                        (3, 500_001, 500_001, False),     # ragged slices
-                                                        (4, 8_000_000, 1_000_000_000, True)])  # C5's filter, 2 ranges
-def test_ipc_or_allreduce_cross_process(oracle, world, n, filter_n, per_sweep):
+@pytest.mark.parametrize("world,n,filter_n,per_sweep,ordered,nseeds",
+                         [(2, 3_000_000, 30_000_000, False, "device", 2),
+                          (3, 500_001, 500_001, False, "device", 2),    # ragged slices
+                          (4, 8_000_000, 1_000_000_000, True, "device", 1),  # C5's filter, 2 ranges
+                          (2, 3_000_000, 30_000_000, False, "host", 2)])
+def test_ipc_or_allreduce_cross_process(oracle, world, n, filter_n, per_sweep, ordered, nseeds):
     """the N > 1 merge without RCCL — `world` processes
     on cuda:0, each exporting its words (lsmb_ipc_export), mapping the others'
     (lsmb_ipc_import) and merging by peer loads (lsmb_or_gather_dev), the path
     `bench.py --backend ipc` times.  RCCL refuses two ranks on one GPU; IPC
     does not, so the cross-process product merge runs here.  Every rank's
-    merged words == the single-process oracle build (digest)."""
+    merged words == the single-process oracle build (digest).
+    VERDICT r04 item 5: ordered="device" orders the merge's phases with flags
+    on the GPUs (lsmb_flag_*): the last rank builds late and the others' merges
+    must wait for it there; a second build + merge on the same words repeats
+    it, and inside that merge the host neither synchronises a stream nor
+    enters a barrier; no flag wait times out."""
     import torch.multiprocessing as mp
     mpc = mp.get_context("spawn")
     q = mpc.Queue()
     port = _free_port()
-    procs = [mpc.Process(target=_ipc_worker, args=(r, world, port, n, filter_n, per_sweep, q)) for r in range(world)]
+    seeds = (0x5EED0001, 0x5EED0003)[:nseeds]
+    procs = [mpc.Process(target=_ipc_worker, args=(r, world, port, n, filter_n, per_sweep, q, ordered, seeds))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in range(world)]
@@ -313,10 +346,13 @@ def test_ipc_or_allreduce_cross_process(oracle, world, n, filter_n, per_sweep):
         p.join(timeout=60)
         assert p.exitcode == 0
     nb, k = lsmbloom.params(filter_n, 0.01)
-    ref = oracle.build_fixed_mt(keygen.key16(0x5EED0001, 0, n), 16, nb, k, 16)
-    for rank, nsw, words in res:
+    refs = [_digest(oracle.build_fixed_mt(keygen.key16(sd, 0, n), 16, nb, k, 16)) for sd in seeds]
+    for rank, nsw, digests, calls, timeouts in res:
         assert nsw == 2 or not per_sweep  # 2 M keys per rank: C5's filter builds in 2 sweeps
-        assert words == _digest(ref), "rank %d merged filter differs" % rank
+        assert digests == refs, "rank %d merged filter differs" % rank
+        assert timeouts == 0
+        if ordered == "device" and nseeds > 1:
+            assert calls == {"sync": 0, "barrier": 0}, calls
 
 
 @pytest.mark.timeout(300)
@@ -345,7 +381,7 @@ def test_bench_launches_its_own_ranks(filter_keys, backend):
         cal = out["step_split"]["overlap_calibration"]
         assert cal["overlapped_ms_per_step"] > 0 and cal["serial_ms_per_step"] > 0
         assert out["step_split"]["timed_step"].startswith("2 build sweeps") == (cal["timed_form"] == "overlapped")
-    assert filter_keys or out["probe"]["member_rows_all_hit"] is True
+    assert filter_keys or out["legs"]["c3_probe"]["member_rows_all_hit"] is True
 
 
 def test_bench_refuses_world_mismatch():

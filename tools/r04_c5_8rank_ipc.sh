@@ -8,13 +8,14 @@
 # single-process rebuild.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-mkdir -p gpurun_out/r04c5
+TAG=${1:-r04c5}
+mkdir -p gpurun_out/$TAG
 ( while sleep 30; do echo tick $(date +%T); done ) &
 TICK=$!
 timeout -k 10 600 python3 bench.py --gpus 8 --backend ipc --steps 2 --warmup 1 --no-probe --no-cpu-baseline --no-e2e \
-  --no-varlen --no-exact10 > gpurun_out/r04c5/c5_8rank_ipc.json 2> gpurun_out/r04c5/c5_8rank_ipc.err
+  --no-varlen --no-exact10 > gpurun_out/$TAG/c5_8rank_ipc.json 2> gpurun_out/$TAG/c5_8rank_ipc.err
 rc=$?
 kill $TICK
 echo "8rank ipc rc=$rc"
-python3 -c 'import json; d=json.load(open("gpurun_out/r04c5/c5_8rank_ipc.json")); print({k: d.get(k) for k in ("n_gpus", "value", "ms_per_step", "words_equal_oracle_fixture", "multi_gpu_merged_equals_single_gpu_build")}, d["step_split"])'
+python3 -c 'import json,sys; d=json.load(open(sys.argv[1])); print({k: d.get(k) for k in ("n_gpus", "value", "ms_per_step", "words_equal_oracle_fixture", "multi_gpu_merged_equals_single_gpu_build")}, d["step_split"])' gpurun_out/$TAG/c5_8rank_ipc.json
 exit $rc
