@@ -43,9 +43,10 @@ def parse():
                     help="keys of the whole run, split over the ranks (default: 1e8 = C2 at N=1, 1e9 = C5 at N>1)")
     ap.add_argument("--keys-per-gpu", type=int, default=0,
                     help="weak scaling instead: this many keys per rank (overrides --global-keys)")
-    ap.add_argument("--backend", default="nccl",
-                    help="N>1 merge: nccl (RCCL collectives), gloo (host-staged), ipc (peer loads over IPC-mapped "
-                         "device words, gloo barriers)")
+    ap.add_argument("--backend", default="auto",
+                    help="N>1 merge: auto (RCCL and IPC both set up; the untimed calibration checks that they agree "
+                         "word for word and times the faster), nccl (RCCL collectives only), gloo (host-staged), "
+                         "ipc (peer loads over IPC-mapped device words, device-ordered phases)")
     ap.add_argument("--probe-keys", type=int, default=10_000_000)
     ap.add_argument("--probe-filters", type=int, default=8)
     ap.add_argument("--no-probe", action="store_true")
@@ -251,17 +252,26 @@ def main():
     from lsmbloom import dist as ldist
 
     ndev = torch.cuda.device_count()
-    if world > 1 and args.backend == "nccl" and world > ndev:
-        print("bench.py: %d RCCL ranks need %d GPUs, %d visible" % (world, world, ndev), file=sys.stderr)
-        sys.exit(2)
+    backend = args.backend
+    if world > 1 and backend in ("nccl", "auto") and world > ndev:
+        if backend == "nccl":
+            print("bench.py: %d RCCL ranks need %d GPUs, %d visible" % (world, world, ndev), file=sys.stderr)
+            sys.exit(2)
+        backend = "ipc"  # ranks sharing a GPU (one-GPU rehearsal): RCCL refuses them, IPC does not
     dev = torch.device("cuda", local % max(1, ndev))
     torch.cuda.set_device(dev)
+    side_group = None  # gloo group of the IPC merge's handle exchange (auto: beside RCCL)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if args.backend == "nccl":
+        if backend in ("nccl", "auto"):
             dist.init_process_group("nccl", device_id=dev)
-        else:  # gloo; ipc: gloo orders the phases, the words move by peer loads
-            dist.init_process_group("gloo" if args.backend == "ipc" else args.backend)
+            if backend == "auto":
+                side_group = dist.new_group(backend="gloo")
+        elif backend == "auto-gloo":  # auto's two-merge path with gloo in RCCL's place (one-GPU tests)
+            dist.init_process_group("gloo")
+            side_group = dist.new_group(backend="gloo")
+        else:  # gloo; ipc: gloo exchanges the handles, the words move by peer loads
+            dist.init_process_group("gloo" if backend == "ipc" else backend)
     ctx = lsmbloom.Context(dev.index)
     # One explicit stream for all of this rank's work: on torch's default (the
     # legacy null) stream, the library maps stream NULL to its context's
@@ -289,7 +299,7 @@ def main():
     keys = torch.empty((npg, 16), dtype=torch.uint8, device=dev)
     ctx.gen_key16_dev(SEED_MEMBERS, lo, npg, keys)
     words = torch.zeros(nw, dtype=torch.int64, device=dev)
-    host_coll = world > 1 and args.backend != "nccl"
+    host_coll = world > 1 and backend not in ("nccl", "auto")
 
     # BloomFilterBuilder::{new, add_key, build} (src/bloom/builder.rs:14-28):
     # lsmb_build_fixed_dev_new writes every word of the filter (output-only
@@ -301,15 +311,37 @@ def main():
         else:
             ctx.build_fixed_dev_new(keys, 16, npg, nb, k, words)
 
-    # --backend ipc: the merge by peer loads over IPC-mapped words (no
-    # collective library on the data path; lsmbloom.dist.IpcMerge)
-    ipc = ldist.IpcMerge(words, ctx) if world > 1 and args.backend == "ipc" else None
-
-    def allreduce():
-        if ipc:
-            ipc.allreduce()
-        elif world > 1:
-            ldist.or_allreduce_(words, ctx=ctx)
+    # The N > 1 merges, each fn(lo, hi, stream) = OR-allreduce of words[lo:hi]
+    # after the stream's pending work:
+    #   rccl  all_to_all reduce-scatter + native OR + all_gather (lsmbloom.dist)
+    #   ipc   peer loads over IPC-mapped words, phases ordered by device flags
+    #         (lsmbloom.dist.IpcMerge; no collective library on the data path)
+    # --backend auto (default) sets up both; the untimed calibration checks that
+    # they merge to the same words and times the faster one.
+    merges, merge_notes, ipc = {}, {}, None
+    if world > 1:
+        if backend in ("nccl", "auto", "gloo", "auto-gloo"):
+            def m_coll(a, b, stream):
+                with torch.cuda.stream(stream):
+                    ldist.or_allreduce_(words[a:b], ctx=ctx)
+            merges["rccl" if backend in ("nccl", "auto") else "gloo"] = m_coll
+        if backend in ("ipc", "auto", "auto-gloo"):
+            err = None
+            try:
+                ipc = ldist.IpcMerge(words, ctx, group=side_group)
+            except Exception as e:  # e.g. no IPC mapping between these GPUs: keep RCCL
+                err = repr(e)[:200]
+            ok = torch.tensor([0 if err else 1], dtype=torch.int32)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=side_group)
+            if int(ok.item()) == 1:
+                merges["ipc"] = lambda a, b, stream: ipc.allreduce(a, b, stream=stream)
+            else:
+                merge_notes["ipc_error"] = err or "failed on another rank"
+                if ipc:
+                    for base in ipc.bases:
+                        ctx.ipc_close(base)
+                    ipc = None
+    form = next(iter(merges), None)
 
     # N > 1 step: the partitioned build runs in sweeps (C5: 2 x 256 MiB word
     # ranges); sweep s's range is final when its pass B ends, so its OR-allreduce
@@ -320,26 +352,22 @@ def main():
     side = torch.cuda.Stream(dev) if overlap else None
     sweep_ev = [torch.cuda.Event() for _ in range(nsw)]
 
-    def step(ov=None):
+    def allreduce(f=None):
+        if world > 1:
+            merges[f or form](0, nw, torch.cuda.current_stream(dev))
+
+    def step(ov=None, f=None):
+        f = f or form
         if not (overlap if ov is None else ov):
             build()
-            allreduce()
+            allreduce(f)
             return
         main = torch.cuda.current_stream(dev)
-        if ipc:  # device-ordered: the merge is only enqueued, the host never waits inside it
-            for s, (a, b) in enumerate(ranges):
-                ctx.build_fixed_dev_sweep_new(keys, 16, npg, nb, k, words, s)
-                sweep_ev[s].record(main)
-                side.wait_event(sweep_ev[s])
-                ipc.allreduce(a, b, stream=side)
-            main.wait_stream(side)
-            return
         for s, (a, b) in enumerate(ranges):
             ctx.build_fixed_dev_sweep_new(keys, 16, npg, nb, k, words, s)
             sweep_ev[s].record(main)
             side.wait_event(sweep_ev[s])
-            with torch.cuda.stream(side):
-                ldist.or_allreduce_(words[a:b], ctx=ctx)
+            merges[f](a, b, side)
         main.wait_stream(side)
 
     def barrier():
@@ -355,27 +383,46 @@ def main():
         return float(t.item())
 
     ctx.set_timing(False)  # no timing markers between the kernels of a timed step
-    for _ in range(args.warmup):
-        step()
+    forms = [(f, ov) for f in (merges or [None]) for ov in ((True, False) if overlap else (False,))]
+    for i in range(args.warmup):
+        step(forms[i % len(forms)][1], forms[i % len(forms)][0])
     barrier()
     calib = None
-    if overlap:
-        # The overlapped collective shares the CUs with pass A, whose workgroups
-        # each need a whole CU's LDS: whether the overlap pays depends on the
-        # node.  Time a few steps each way (untimed for the metric; the max over
-        # ranks, so every rank picks the same) and time the faster form.
-        def timed(ov, reps):
+    if world > 1 and len(merges) > 1:
+        # The merges must agree word for word (one serial step each, untimed)
+        # before either is timed; if they do not, RCCL is kept.
+        snaps = {}
+        for f in merges:
+            step(False, f)
+            barrier()
+            snaps[f] = words.clone()
+        names = list(snaps)
+        agree = all(torch.equal(snaps[names[0]], snaps[x]) for x in names[1:])
+        del snaps
+        t = torch.tensor([1 if agree else 0], dtype=torch.int32, device=dev if not host_coll else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        merge_notes["merges_agree"] = bool(t.item())
+        if not merge_notes["merges_agree"]:
+            forms = [x for x in forms if x[0] != "ipc"]
+    if len(forms) > 1:
+        # Overlapped vs serial and RCCL vs IPC: the overlapped collective shares
+        # the CUs with pass A, whose workgroups each need a whole CU's LDS, and
+        # the merges' speed depends on the node's links.  Time a few steps of
+        # each form (untimed for the metric; the max over ranks, so every rank
+        # picks the same) and time the fastest.
+        def timed(f, ov, reps):
             barrier()
             t = time.perf_counter()
             for _ in range(reps):
-                step(ov)
+                step(ov, f)
             barrier()
             return max_over_ranks(time.perf_counter() - t) / reps * 1e3
         reps = max(2, min(5, args.steps))
-        t_ov, t_ser = timed(True, reps), timed(False, reps)
-        overlap = t_ov <= t_ser
-        calib = {"overlapped_ms_per_step": round(t_ov, 4), "serial_ms_per_step": round(t_ser, 4),
-                 "steps_each": reps, "timed_form": "overlapped" if overlap else "serial"}
+        cal = {(f, ov): timed(f, ov, reps) for f, ov in forms}
+        form, overlap = min(cal, key=cal.get)
+        calib = {"%s_%s_ms_per_step" % (f, "overlapped" if ov else "serial"): round(v, 4)
+                 for (f, ov), v in cal.items()}
+        calib.update({"steps_each": reps, "timed_form": "overlapped" if overlap else "serial", "timed_merge": form})
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -444,22 +491,21 @@ def main():
     out["roofline"] = roof
     if world > 1:
         moved = 2 * (world - 1) / world * 8 * nw
-        out["config"]["backend"] = args.backend
+        out["config"]["backend"] = backend
+        merge_what = {"ipc": "ipc: peer loads over IPC-mapped words (OR gather reduce-scatter + copy all-gather), "
+                             "phases ordered by device flags",
+                      "rccl": "rccl: all_to_all reduce-scatter + native OR kernel + all_gather",
+                      "gloo": "gloo: host-staged collectives + native OR kernel"}
         out["step_split"] = {"build_ms": round(build_ms, 4), "or_allreduce_ms": round(coll_ms, 4),
                              "what": "serial steps (untimed pass), slowest rank: device build (fresh) / "
-                                     + ("bitwise-OR allreduce by peer loads over IPC-mapped words (OR gather "
-                                        "reduce-scatter + copy all-gather, phases ordered by device flags)"
-                                        if ipc else
-                                        "bitwise-OR allreduce (all_to_all reduce-scatter + native OR kernel "
-                                        "+ all_gather)") + " of the whole filter",
+                                     "bitwise-OR allreduce of the whole filter (%s)" % merge_what.get(form, form),
                              "serial_ms_per_step": round(serial_ms, 4),
                              "overlap_calibration": calib,
                              "timed_step": ("%d build sweeps, each sweep's word range OR-allreduced on a side "
                                             "stream while the next sweep builds" % nsw) if overlap
                                            else "build then OR-allreduce",
-                             "merge": ("ipc (peer loads, device-ordered flags)" if ipc else
-                                       "rccl all_to_all + OR kernel + all_gather" if args.backend == "nccl" else
-                                       "%s collectives (host-staged) + OR kernel" % args.backend),
+                             "merge": form,
+                             "merges_available": list(merges),
                              "or_allreduce_bytes_per_gpu": int(moved),
                              "or_allreduce_GBs_per_gpu": round(moved / (coll_ms * 1e-3) / 1e9, 1) if coll_ms else None}
         # Self-check (outside the timed region): one more sharded step; rank 0
@@ -493,6 +539,7 @@ def main():
         if ipc:
             torch.cuda.synchronize(dev)
             out["step_split"]["flag_timeouts"] = int(max_over_ranks(ipc.timeouts()))
+        out["step_split"].update(merge_notes)
         dist.barrier()
 
     # Full-size parity in the bench line itself: the filter the timed steps built
@@ -609,7 +656,8 @@ def compact_line(out):
         ss = out["step_split"]
         c["step_split"] = {k: ss.get(k) for k in ("build_ms", "or_allreduce_ms", "serial_ms_per_step",
                                                   "or_allreduce_bytes_per_gpu", "or_allreduce_GBs_per_gpu",
-                                                  "overlap_calibration", "timed_step", "merge", "flag_timeouts")}
+                                                  "overlap_calibration", "timed_step", "merge", "merges_available",
+                                                  "merges_agree", "ipc_error", "flag_timeouts")}
     if "single_gpu_same_workload" in out:
         sg = out["single_gpu_same_workload"]
         c["single_gpu_same_workload"] = {"ms": sg.get("ms"), "value": sg.get("value")}

@@ -356,7 +356,8 @@ def test_ipc_or_allreduce_cross_process(oracle, world, n, filter_n, per_sweep, o
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("filter_keys,backend", [(None, "gloo"), (1_000_000_000, "gloo"), (1_000_000_000, "ipc")])
+@pytest.mark.parametrize("filter_keys,backend", [(None, "gloo"), (1_000_000_000, "gloo"), (1_000_000_000, "ipc"),
+                                                 (1_000_000_000, "auto-gloo")])
 def test_bench_launches_its_own_ranks(filter_keys, backend):
     """`python bench.py --gpus 2` (no torchrun) starts two ranks itself; here
     over gloo, both on cuda:0.  The line must say n_gpus 2, carry the split
@@ -379,8 +380,16 @@ def test_bench_launches_its_own_ranks(filter_keys, backend):
     assert out["step_split"]["or_allreduce_ms"] > 0 and out["step_split"]["build_ms"] > 0
     if filter_keys:  # overlapped vs serial steps timed first; the faster form is the timed one
         cal = out["step_split"]["overlap_calibration"]
-        assert cal["overlapped_ms_per_step"] > 0 and cal["serial_ms_per_step"] > 0
+        merges = out["step_split"]["merges_available"]
+        assert set(merges) == ({"gloo", "ipc"} if backend == "auto-gloo" else {backend})
+        for m in merges:
+            assert cal["%s_overlapped_ms_per_step" % m] > 0 and cal["%s_serial_ms_per_step" % m] > 0
+        assert cal["timed_merge"] == out["step_split"]["merge"] in merges
         assert out["step_split"]["timed_step"].startswith("2 build sweeps") == (cal["timed_form"] == "overlapped")
+        if backend == "auto-gloo":  # both merges ran, agreed word for word, the faster was timed
+            assert out["step_split"]["merges_agree"] is True
+        if "ipc" in merges:
+            assert out["step_split"]["flag_timeouts"] == 0
     assert filter_keys or out["legs"]["c3_probe"]["member_rows_all_hit"] is True
 
 
