@@ -467,11 +467,9 @@ def main():
     roof.update({"algorithmic_bytes_per_key": round(alg_bytes / npg, 3), "pass_a_ms": round(float(kt[1]), 4),
                  "pass_b_ms": round(float(kt[2]), 4)})
     if world == 1 and npg == 100_000_000:
-        roof["hash_walk_floor"] = {
-            "ms": HASH_WALK_FLOOR_MS_PER_1E8, "frac_of_hbm_roofline_at_that_time": round(
-                alg_bytes / (HASH_WALK_FLOOR_MS_PER_1E8 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "what": "XXH3-128 + 7 exact positions of 100 M 16-B keys alone, full occupancy (tools/mb_hash.hip): "
-                    "no build can beat this compute floor"}
+        roof["hash_walk_floor"] = dict(HASH_WALK_FLOOR, frac_of_hbm_roofline_at_that_time=round(
+            alg_bytes / (HASH_WALK_FLOOR["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
+        roof["hash_walk_floor"]["phase"] = PASS_A_PHASE
 
     out = {"metric": "bloom build + batched probe, Mkeys/s device-resident, at 1/2/4/8 MI355X",
            "value": round(value, 2), "unit": "Mkeys/s", "n_gpus": world, "steps": args.steps,
@@ -644,9 +642,10 @@ def compact_line(out):
         if k in roof:
             r[k] = roof[k]
     if "hash_walk_floor" in roof:
-        r["hash_walk_floor_ms"] = roof["hash_walk_floor"].get("ms")
-        if "phase" in roof["hash_walk_floor"]:
-            r["phase"] = roof["hash_walk_floor"]["phase"]
+        hw = roof["hash_walk_floor"]
+        r["hash_walk_floor_ms"] = {k: hw.get(k) for k in ("ms", "pass_a_geometry_ms", "with_claims_and_slot_writes_ms")}
+        if "phase" in hw:
+            r["pass_a_phase"] = {k: v for k, v in hw["phase"].items() if k != "source"}
     c["roofline"] = r
     for k in ("words_equal_oracle_fixture", "multi_gpu_merged_equals_single_gpu_build", "multi_gpu_check_error",
               "verified_bit_exact"):
@@ -1017,7 +1016,22 @@ def committed_legs():
 # LDS: SQ_LDS_IDX_ACTIVE = LDS-array cycles over the 256 CUs' LDS.
 VALU_CYCLES_PER_INST = 4.0
 SATURATED = 0.75  # a unit busier than this fraction of the launch's cycles is its limiter
-HASH_WALK_FLOOR_MS_PER_1E8 = 0.47  # XXH3-128 of 16-B keys + 7 exact positions, full occupancy (tools/mb_hash.hip)
+# The C2 compute floor, re-measured on the round-5 arithmetic (tools/mb_hash.hip,
+# profiles/r05/r05a_hash_floor.log): XXH3-128 of 100 M 16-B keys + their 7 exact
+# positions, k = 7 unrolled, at full occupancy; the same at pass A's geometry
+# (1024-thread workgroups, one per CU), and with pass A's claims and ring slot
+# writes added (no flush, no barriers).
+HASH_WALK_FLOOR = {"ms": 0.354, "pass_a_geometry_ms": 0.404, "with_claims_and_slot_writes_ms": 0.538,
+                   "source": "profiles/r05/r05a_hash_floor.log",
+                   "what": "no build can beat the hash + position arithmetic alone"}
+# Where pass A's phase goes (LSMB_STAMP build, profiles/r05/r05e_stamps.log;
+# shares of the cycles per phase per wave) and the ablations around it
+# (tools/build_variants.sh + run_variants.sh, profiles/r05/r05e_passA_ablations.log:
+# pass A ms with no flush / no region stores / every region store dropped).
+PASS_A_PHASE = {"cycles": 6228, "work": 0.356, "barrier1": 0.169, "flush": 0.322, "barrier2": 0.152,
+                "ablation_pass_a_ms": {"product": 0.980, "no_flush": 0.570, "no_region_stores": 0.733,
+                                       "stores_dropped": 0.857},
+                "source": "profiles/r05/r05e_stamps.log, r05e_passA_ablations.log"}
 
 
 def native_record():

@@ -65,6 +65,41 @@ __global__ __launch_bounds__(256) void k_op(uint32_t seed, uint32_t* out, unsign
             if constexpr (OP == 17) asm volatile("v_mul_f32 %0, %0, %1" : "+v"(a[c]) : "v"(b));
             if constexpr (OP == 18) asm volatile("v_lshrrev_b64 %0, 3, %0" : "+v"(A[c]));
             if constexpr (OP == 19) asm volatile("v_bfe_u32 %0, %0, 3, 20" : "+v"(a[c]));
+            // round 5: the rest of the per-key instruction mix, and encodings
+            if constexpr (OP == 20) OP_V32("v_and_b32");
+            if constexpr (OP == 21) OP_V32("v_or_b32");
+            if constexpr (OP == 22) OP_V32("v_sub_u32");
+            if constexpr (OP == 23) OP_V32("v_lshlrev_b32");
+            if constexpr (OP == 24) OP_V32("v_lshrrev_b32");
+            if constexpr (OP == 25) asm volatile("v_mov_b32 %0, %1" : "=v"(a[c]) : "v"(a[(c + 3) & 7]));
+            if constexpr (OP == 26) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a[c]) : "v"(b) : "vcc");
+            if constexpr (OP == 27) asm volatile("v_lshl_or_b32 %0, %0, 3, %1" : "+v"(a[c]) : "v"(b));
+            if constexpr (OP == 28) asm volatile("v_lshl_add_u32 %0, %0, 3, %1" : "+v"(a[c]) : "v"(b));
+            if constexpr (OP == 29) asm volatile("v_perm_b32 %0, %0, %1, %1" : "+v"(a[c]) : "v"(b));
+            if constexpr (OP == 30) asm volatile("v_mad_u32_u24 %0, %0, %1, %1" : "+v"(a[c]) : "v"(b));
+            if constexpr (OP == 31) OP_V32("v_max_u32");
+            if constexpr (OP == 32) asm volatile("v_bfi_b32 %0, %0, %1, %1" : "+v"(a[c]) : "v"(b));
+            if constexpr (OP == 33) asm volatile("v_add_co_u32 %0, vcc, %0, %1" : "+v"(a[c]) : "v"(b) : "vcc");
+            if constexpr (OP == 34) asm volatile("v_sub_co_u32 %0, vcc, %0, %1" : "+v"(a[c]) : "v"(b) : "vcc");
+            if constexpr (OP == 35) asm volatile("v_cmp_gt_u32 vcc, %0, %1" : : "v"(a[c]), "v"(b) : "vcc");
+            if constexpr (OP == 36) asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(a[c]) : "v"(b));
+            if constexpr (OP == 37) asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(A[c]) : "v"(B));
+            if constexpr (OP == 38) asm volatile("v_pk_fma_f32 %0, %0, %1, %1" : "+v"(A[c]) : "v"(B));
+            if constexpr (OP == 39) asm volatile("v_cvt_u32_f32 %0, %0" : "+v"(a[c]));
+            if constexpr (OP == 40) asm volatile("v_max3_u32 %0, %0, %1, %1" : "+v"(a[c]) : "v"(b));
+            if constexpr (OP == 41) OP_V32("v_ashrrev_i32");
+            if constexpr (OP == 42) asm volatile("v_add_u32 %0, 0x12345, %0" : "+v"(a[c]));
+            if constexpr (OP == 43) asm volatile("v_xor_b32_e64 %0, %0, %1" : "+v"(a[c]) : "v"(b));
+            if constexpr (OP == 44) asm volatile("v_min_u32_e64 %0, %0, %1" : "+v"(a[c]) : "v"(b));
+            if constexpr (OP == 45) asm volatile("v_subrev_u32 %0, %1, %0" : "+v"(a[c]) : "v"(b));
+            if constexpr (OP == 46) asm volatile("v_and_or_b32 %0, %0, %1, %1" : "+v"(a[c]) : "v"(b));
+            if constexpr (OP == 47) asm volatile("v_bitop3_b32 %0, %0, %1, %1 bitop3:0x80" : "+v"(a[c]) : "v"(b));
+            if constexpr (OP == 48) asm volatile("v_xad_u32 %0, %0, %1, %1" : "+v"(a[c]) : "v"(b));
+            if constexpr (OP == 49) asm volatile("v_addc_co_u32 %0, vcc, %0, %1, vcc" : "+v"(a[c]) : "v"(b) : "vcc");
+            if constexpr (OP == 50) asm volatile("v_add_f32 %0, %0, %1" : "+v"(a[c]) : "v"(b));
+            if constexpr (OP == 51) asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(A[c]) : "v"(B));
+            if constexpr (OP == 52) asm volatile("v_med3_u32 %0, %0, %1, %1" : "+v"(a[c]) : "v"(b));
+            if constexpr (OP == 53) asm volatile("v_mul_hi_u32_u24 %0, %0, %1" : "+v"(a[c]) : "v"(b));
         }
     }
     const uint64_t t1 = __builtin_amdgcn_s_memtime();
@@ -79,8 +114,19 @@ static const char* kNames[] = {"v_xor_b32",      "v_add_u32",        "v_mul_u32_
                                "v_mul_hi_u32",   "v_mad_u64_u32",    "v_lshl_add_u64",      "v_cmp_lt_u64+cndmask",
                                "v_add_co+addc",  "v_cvt_f64_u32",    "v_mul_f64",           "v_fma_f64",
                                "v_cvt_u32_f64",  "v_alignbit_b32",   "v_add3_u32",          "v_min_u32",
-                               "v_cvt_f32_u32",  "v_mul_f32",        "v_lshrrev_b64",       "v_bfe_u32"};
-static const int kInsnPerOp[] = {1, 1, 1, 1, 1, 1, 1, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1};
+                               "v_cvt_f32_u32",  "v_mul_f32",        "v_lshrrev_b64",       "v_bfe_u32",
+                               "v_and_b32",      "v_or_b32",         "v_sub_u32",           "v_lshlrev_b32",
+                               "v_lshrrev_b32",  "v_mov_b32",        "v_cndmask_b32(vcc)",  "v_lshl_or_b32",
+                               "v_lshl_add_u32", "v_perm_b32",       "v_mad_u32_u24",       "v_max_u32",
+                               "v_bfi_b32",      "v_add_co_u32",     "v_sub_co_u32",        "v_cmp_gt_u32(e32)",
+                               "v_fma_f32",      "v_pk_add_f32",     "v_pk_fma_f32",        "v_cvt_u32_f32",
+                               "v_max3_u32",     "v_ashrrev_i32",    "v_add_u32(literal)",  "v_xor_b32_e64",
+                               "v_min_u32_e64",  "v_subrev_u32",     "v_and_or_b32",        "v_bitop3_b32",
+                               "v_xad_u32",      "v_addc_co_u32",    "v_add_f32",           "v_pk_mul_f32",
+                               "v_med3_u32",     "v_mul_hi_u32_u24"};
+static const int kInsnPerOp[] = {1, 1, 1, 1, 1, 1, 1, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1};
 
 template <int OP>
 void run(int wps, uint32_t* out, unsigned long long* cyc, int ncu) {
@@ -112,18 +158,21 @@ void run(int wps, uint32_t* out, unsigned long long* cyc, int ncu) {
 }
 
 template <int... OPS>
-void run_all(int wps, uint32_t* out, unsigned long long* cyc, int ncu, std::integer_sequence<int, OPS...>) {
-    (run<OPS>(wps, out, cyc, ncu), ...);
+void run_all(int wps, uint32_t* out, unsigned long long* cyc, int ncu, int first, std::integer_sequence<int, OPS...>) {
+    ((OPS >= first ? run<OPS>(wps, out, cyc, ncu) : void()), ...);
 }
 
-int main() {
+int main(int argc, char** argv) {
     int ncu = 0;
     CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
     uint32_t* out;
     unsigned long long* cyc;
     CK(hipMalloc(&out, (size_t)ncu * 4 * 8 * 64 * 4));
     CK(hipMalloc(&cyc, 8));
-    for (int wps : {4, 8}) run_all(wps, out, cyc, ncu, std::make_integer_sequence<int, 20>{});
+    const int nops = argc > 1 ? atoi(argv[1]) : 54;  // ops [first, 54): argv[2]
+    const int first = argc > 2 ? atoi(argv[2]) : 0;
+    (void)nops;
+    for (int wps : {4, 8}) run_all(wps, out, cyc, ncu, first, std::make_integer_sequence<int, 54>{});
     CK(hipFree(out));
     CK(hipFree(cyc));
     return 0;
