@@ -383,14 +383,16 @@ def main():
         return float(t.item())
 
     ctx.set_timing(False)  # no timing markers between the kernels of a timed step
-    forms = [(f, ov) for f in (merges or [None]) for ov in ((True, False) if overlap else (False,))]
-    for i in range(args.warmup):
-        step(forms[i % len(forms)][1], forms[i % len(forms)][0])
-    barrier()
     calib = None
+    if ipc is not None:
+        # A merge takes milliseconds: a phase wait this long means a peer never
+        # signalled (or its flags are not visible here); the merge is then
+        # dropped below instead of stalling every step.
+        ipc.timeout_ms = 3000
     if world > 1 and len(merges) > 1:
-        # The merges must agree word for word (one serial step each, untimed)
-        # before either is timed; if they do not, RCCL is kept.
+        # The merges must agree word for word (one serial step each, untimed,
+        # before any warm-up) and the IPC merge's waits must all have been
+        # met; otherwise only RCCL is timed.
         snaps = {}
         for f in merges:
             step(False, f)
@@ -399,11 +401,19 @@ def main():
         names = list(snaps)
         agree = all(torch.equal(snaps[names[0]], snaps[x]) for x in names[1:])
         del snaps
+        if ipc is not None and ipc.timeouts():
+            agree = False
+            merge_notes["ipc_error"] = "flag waits timed out in the agreement step"
         t = torch.tensor([1 if agree else 0], dtype=torch.int32, device=dev if not host_coll else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         merge_notes["merges_agree"] = bool(t.item())
         if not merge_notes["merges_agree"]:
-            forms = [x for x in forms if x[0] != "ipc"]
+            merges.pop("ipc", None)
+            form = next(iter(merges))
+    forms = [(f, ov) for f in (merges or [None]) for ov in ((True, False) if overlap else (False,))]
+    for i in range(args.warmup):
+        step(forms[i % len(forms)][1], forms[i % len(forms)][0])
+    barrier()
     if len(forms) > 1:
         # Overlapped vs serial and RCCL vs IPC: the overlapped collective shares
         # the CUs with pass A, whose workgroups each need a whole CU's LDS, and
@@ -536,7 +546,7 @@ def main():
                 out["multi_gpu_check_error"] = repr(e)[:200]
         if ipc:
             torch.cuda.synchronize(dev)
-            out["step_split"]["flag_timeouts"] = int(max_over_ranks(ipc.timeouts()))
+            out["step_split"]["flag_timeouts"] = int(max_over_ranks(float(ipc.timeouts())))
         out["step_split"].update(merge_notes)
         dist.barrier()
 
@@ -580,7 +590,7 @@ def main():
         out["detail"] = write_detail(out, args.detail_out)
         print(json.dumps(compact_line(out), separators=(",", ":")), flush=True)
     if ipc:
-        ipc.close()
+        ipc.close(check=False)  # (timeouts, if any, are in step_split.flag_timeouts)
     ctx.close()
     if world > 1:
         dist.destroy_process_group()

@@ -33,6 +33,10 @@ namespace lsmb {
 namespace {
 
 constexpr uint32_t kProbeTableBytes = 64 * 1024;  // bit-sliced tables: the launchers' LDS cap
+#ifndef LSMB_PROBE_DEPTH
+#define LSMB_PROBE_DEPTH 3
+#endif
+constexpr int kProbeDepth = LSMB_PROBE_DEPTH;  // C3 probe: rounds of keys in flight
 
 using ks::Fixed16;
 using ks::FixedN;
@@ -127,12 +131,12 @@ __global__ __launch_bounds__(BS) void k_probe_sliced(Src src, uint64_t n, typena
     // SIMD) to arrive.  The scheduling barriers keep the rounds in program
     // order: left alone, the scheduler interleaves the three independent
     // rounds and the loop head then waits for every load.
-    u32x4 ka = round_keys(0);
-    __builtin_amdgcn_sched_barrier(0);
-    u32x4 kb = round_keys(1);
-    __builtin_amdgcn_sched_barrier(0);
-    u32x4 kc = round_keys(2);
-    __builtin_amdgcn_sched_barrier(0);
+    u32x4 kr[kProbeDepth];
+#pragma unroll
+    for (int d = 0; d < kProbeDepth; d++) {
+        kr[d] = round_keys(d);
+        __builtin_amdgcn_sched_barrier(0);
+    }
     const uint32_t nw32 = (uint32_t)(((uint64_t)num_bits + 31) / 32);  // 64-bit: num_bits may be 2^32-1
     // The filters' word pointers and output bits, loaded once and all at
     // once (a per-filter descriptor -> word load chain would serialise 2F
@@ -204,18 +208,14 @@ __global__ __launch_bounds__(BS) void k_probe_sliced(Src src, uint64_t n, typena
             }
             __builtin_amdgcn_raw_buffer_store_b8(m, R.rsrc(out, j, 1), R.lane, 0, 2 /* nt */);
         };
-        for (uint32_t j = 0; j < R.rounds; j += 3) {  // past the last round: empty windows (zeros, dropped rows)
-            row(ka, j);
-            __builtin_amdgcn_sched_barrier(0);
-            ka = round_keys(j + 3);
-            if (j + 1 == R.rounds) return;
-            row(kb, j + 1);
-            __builtin_amdgcn_sched_barrier(0);
-            kb = round_keys(j + 4);
-            if (j + 2 == R.rounds) return;
-            row(kc, j + 2);
-            __builtin_amdgcn_sched_barrier(0);
-            kc = round_keys(j + 5);
+        for (uint32_t j = 0; j < R.rounds; j += kProbeDepth) {  // past the last round: empty windows (zeros, dropped rows)
+#pragma unroll
+            for (int d = 0; d < kProbeDepth; d++) {
+                row(kr[d], j + d);
+                __builtin_amdgcn_sched_barrier(0);
+                kr[d] = round_keys(j + d + kProbeDepth);
+                if (j + d + 1 == R.rounds) return;
+            }
         }
         return;
     }
