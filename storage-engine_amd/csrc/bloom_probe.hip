@@ -34,7 +34,7 @@ namespace {
 
 constexpr uint32_t kProbeTableBytes = 64 * 1024;  // bit-sliced tables: the launchers' LDS cap
 #ifndef LSMB_PROBE_DEPTH
-#define LSMB_PROBE_DEPTH 3
+#define LSMB_PROBE_DEPTH 5
 #endif
 constexpr int kProbeDepth = LSMB_PROBE_DEPTH;  // C3 probe: rounds of keys in flight
 
@@ -126,11 +126,13 @@ __global__ __launch_bounds__(BS) void k_probe_sliced(Src src, uint64_t n, typena
         else
             return u32x4{0, 0, 0, 0};
     };
-    // Three rounds in flight: round j + 3 is requested once round j is done,
-    // so each load has two rounds of hashing (~4 K cycles at 4 waves per
-    // SIMD) to arrive.  The scheduling barriers keep the rounds in program
-    // order: left alone, the scheduler interleaves the three independent
-    // rounds and the loop head then waits for every load.
+    // kProbeDepth (5) rounds in flight: round j + 5 is requested once round j
+    // is done, so each load has four rounds of hashing to arrive (3 rounds:
+    // 0.0423-0.0428 ms per C3 batch, 4: 0.0428-0.043, 5: 0.0411-0.0413,
+    // 6: 0.0433; profiles/r05/r05g_probe_depth_pipe_ab.log, r05f).  The
+    // scheduling barriers keep the rounds in program order: left alone, the
+    // scheduler interleaves the independent rounds and the loop head then
+    // waits for every load.
     u32x4 kr[kProbeDepth];
 #pragma unroll
     for (int d = 0; d < kProbeDepth; d++) {
