@@ -42,9 +42,6 @@
 #ifndef LSMB_ABL
 #define LSMB_ABL 0
 #endif
-#ifndef LSMB_STORE_AUX
-#define LSMB_STORE_AUX 0  // pass A region stores' cache policy bits (measurement variants)
-#endif
 #ifndef LSMB_APPLY_U
 #define LSMB_APPLY_U 8  // pass B: 16-B region loads in flight per lane
 #endif
@@ -481,10 +478,10 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
             const uint2 q4 = pack3w<SL>(x1.x, y1.x, z1.x), q5 = pack3w<SL>(x1.y, y1.y, z1.y);
             const uint2 q6 = pack3w<SL>(x1.z, y1.z, z1.z), q7 = pack3w<SL>(x1.w, y1.w, z1.w);
             if (!(LSMB_ABL & 8)) {
-                __builtin_amdgcn_raw_buffer_store_b128(u32x4{q0.x, q0.y, q1.x, q1.y}, rgn, off, 0, LSMB_STORE_AUX);
-                __builtin_amdgcn_raw_buffer_store_b128(u32x4{q2.x, q2.y, q3.x, q3.y}, rgn, off + 16, 0, LSMB_STORE_AUX);
-                __builtin_amdgcn_raw_buffer_store_b128(u32x4{q4.x, q4.y, q5.x, q5.y}, rgn, off + 32, 0, LSMB_STORE_AUX);
-                __builtin_amdgcn_raw_buffer_store_b128(u32x4{q6.x, q6.y, q7.x, q7.y}, rgn, off + 48, 0, LSMB_STORE_AUX);
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{q0.x, q0.y, q1.x, q1.y}, rgn, off, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{q2.x, q2.y, q3.x, q3.y}, rgn, off + 16, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{q4.x, q4.y, q5.x, q5.y}, rgn, off + 32, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{q6.x, q6.y, q7.x, q7.y}, rgn, off + 48, 0, 0);
             }
         };
         auto spill_segment = [&]() {  // region full (adversarial inputs): exact global atomics
@@ -545,7 +542,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(Src src, uint64_t n, Mod32 md
                 w1 = pack3w<SL>(a0.y, a1.y, a2.y);
                 off = (LSMB_ABL & 16) ? kDrop : jb.w + 16 * l;
             }
-            if (!(LSMB_ABL & 8)) __builtin_amdgcn_raw_buffer_store_b128(u32x4{w0.x, w0.y, w1.x, w1.y}, rgn, off, 0, LSMB_STORE_AUX);
+            if (!(LSMB_ABL & 8)) __builtin_amdgcn_raw_buffer_store_b128(u32x4{w0.x, w0.y, w1.x, w1.y}, rgn, off, 0, 0);
         }
         // 3. owners advance past the posted segment; the rest per lane
         if (has) {

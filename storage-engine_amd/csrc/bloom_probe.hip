@@ -25,9 +25,6 @@
 #include "kernels.hpp"
 #include "keysrc.hpp"
 
-#ifndef LSMB_PROBE_ABL
-#define LSMB_PROBE_ABL 0  // measurement variants (tools/build_probe_variants.sh); 0 = the product
-#endif
 
 namespace lsmb {
 namespace {
@@ -227,23 +224,13 @@ __global__ __launch_bounds__(BS) void k_probe_sliced(Src src, uint64_t n, typena
     for (; i < n; i += gs) {
         const typename Src::Pre cur = pre;
         pre = src.fetch(i + gs, i + gs < n);
-        H128 h;
-        if constexpr (LSMB_PROBE_ABL == 2 && std::is_same<Src, Fixed16>::value)  // variant: no XXH3 (raw key words)
-            h = H128{((uint64_t)cur.y << 32) | cur.x, ((uint64_t)cur.w << 32) | cur.z};
-        else
-            h = src.hash_pre(cur, i);
+        const H128 h = src.hash_pre(cur, i);
         W pw(md, h.lo, h.hi);
         T m = all;
         if (K > 0) {
 #pragma unroll
             for (int j = 0; j < K; j++) {
-#if LSMB_PROBE_ABL == 1  // measurement variant: no table reads
-                m ^= (T)pw.pos();
-#elif LSMB_PROBE_ABL == 3  // measurement variant: no position walk (table reads at hash bits)
-                m &= table[(uint32_t)(h.lo >> (5 * j)) & 8191u];
-#else
                 m &= table[pw.pos()];
-#endif
                 if (j + 1 < K) pw.next(md);
             }
         } else {
