@@ -351,12 +351,21 @@ int lsmb_ipc_close(lsmb_ctx* ctx, void* d_base);
 int lsmb_or_gather_dev(lsmb_ctx* ctx, void* d_dst, const void* const* d_srcs, uint32_t nsrc, uint64_t nwords,
                        void* stream);
 
+/* The merge's all-gather in one call: for every slice r < nsrc with
+ * d_srcs[r] != NULL, d_dst[w] = d_srcs[r][w] for w in [r slice_words,
+ * min((r+1) slice_words, nwords)) (u64 words; a NULL source leaves its slice
+ * alone, e.g. the caller's own).  One kernel streams every slice at once, so
+ * every peer link is busy.  The sources (mapped peer memory, or other local
+ * buffers) must not overlap d_dst.  Asynchronous on `stream`. */
+int lsmb_copy_slices_dev(lsmb_ctx* ctx, void* d_dst, const void* const* d_srcs, uint32_t nsrc, uint64_t slice_words,
+                         uint64_t nwords, void* stream);
+
 /* Device-ordered phases for the merge above, so that no host waits inside it:
  * a flag is a u32 epoch counter in device memory (this process's own, or a
  * peer's mapped with lsmb_ipc_import).  The merge of epoch e on `stream` is
  *   signal(own flag[0], e); wait(every rank's flag[0] >= e)   partials final
  *   or_gather (reduce-scatter);  signal(flag[1], e); wait(all flag[1] >= e)
- *   or_gather copies (all-gather); signal(flag[2], e); wait(all flag[2] >= e)
+ *   copy_slices (all-gather); signal(flag[2], e); wait(all flag[2] >= e)
  * (lsmbloom.dist.IpcMerge).  All enqueue and return at once. */
 
 /* After everything before it on `stream`: a system-scope release store of

@@ -44,22 +44,55 @@ struct OrSources {
 // dst[i] = OR over j of src_j[i], i < count (elements of V).  dst may be one
 // of the sources (the owner's own partial): each element is read by every
 // source load before its one store, by the same thread.  So dst is not
-// __restrict__ (it aliases a source).
-template <class V>
+// __restrict__ (it aliases a source).  N > 0: N sources known at compile
+// time, so a thread's N loads (over N peer links) are all in flight before
+// the first OR; N = 0: a runtime count (9..16 sources).
+template <class V, int N>
 __global__ __launch_bounds__(256) void k_or_gather(V* dst, OrSources src, uint64_t count) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    auto orv = [](V& v, const V& x) {
+        if constexpr (sizeof(V) == 16) {
+            v.x |= x.x, v.y |= x.y, v.z |= x.z, v.w |= x.w;
+        } else {
+            v |= x;
+        }
+    };
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
         V v = static_cast<const V*>(src.p[0])[i];
-        for (uint32_t j = 1; j < src.n; j++) {
-            const V w = static_cast<const V*>(src.p[j])[i];
-            if constexpr (sizeof(V) == 16) {
-                v.x |= w.x, v.y |= w.y, v.z |= w.z, v.w |= w.w;
-            } else {
-                v |= w;
-            }
+        if constexpr (N > 0) {
+            V w[N];
+#pragma unroll
+            for (int j = 1; j < N; j++) w[j] = static_cast<const V*>(src.p[j])[i];
+#pragma unroll
+            for (int j = 1; j < N; j++) orv(v, w[j]);
+        } else {
+            for (uint32_t j = 1; j < src.n; j++) orv(v, static_cast<const V*>(src.p[j])[i]);
         }
         dst[i] = v;
     }
+}
+
+// The all-gather of a merge in one kernel: dst[i] = src_r[i] for every
+// element of slice r = [r per, min((r+1) per, count)) whose source is set
+// (src.p[r] == nullptr: the caller's own slice, left alone).  blockIdx.y is
+// the slice, so every peer link streams at once (one copy per peer, one
+// after another on a stream, would use one link at a time).  Four elements
+// in flight per thread.
+template <class V>
+__global__ __launch_bounds__(256) void k_copy_slices(V* __restrict__ dst, OrSources src, uint64_t per, uint64_t count) {
+    const V* __restrict__ s = static_cast<const V*>(src.p[blockIdx.y]);
+    if (!s) return;  // (block-uniform)
+    const uint64_t a = (uint64_t)blockIdx.y * per, b = min(count, a + per);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = a + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < b; i += 4 * stride) {
+        V x[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) x[u] = s[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < 4; u++) dst[i + u * stride] = x[u];
+    }
+    for (; i < b; i += stride) dst[i] = s[i];
 }
 
 // ---- device-ordered phase flags (cross-process merge, lsmb_flag_*) --------
@@ -99,6 +132,23 @@ __global__ __launch_bounds__(64) void k_flag_wait(FlagSet fs, uint32_t value, ui
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: later reads see the peers' data
 }
 
+template <class V>
+hipError_t or_gather_n(V* dst, const OrSources& s, uint64_t count, uint32_t g, hipStream_t st) {
+    const dim3 grid(g), block(256);
+    switch (s.n) {
+        case 1: k_or_gather<V, 1><<<grid, block, 0, st>>>(dst, s, count); break;
+        case 2: k_or_gather<V, 2><<<grid, block, 0, st>>>(dst, s, count); break;
+        case 3: k_or_gather<V, 3><<<grid, block, 0, st>>>(dst, s, count); break;
+        case 4: k_or_gather<V, 4><<<grid, block, 0, st>>>(dst, s, count); break;
+        case 5: k_or_gather<V, 5><<<grid, block, 0, st>>>(dst, s, count); break;
+        case 6: k_or_gather<V, 6><<<grid, block, 0, st>>>(dst, s, count); break;
+        case 7: k_or_gather<V, 7><<<grid, block, 0, st>>>(dst, s, count); break;
+        case 8: k_or_gather<V, 8><<<grid, block, 0, st>>>(dst, s, count); break;
+        default: k_or_gather<V, 0><<<grid, block, 0, st>>>(dst, s, count); break;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_or_gather(uint64_t* dst, const OrSources& s, uint64_t nwords, int num_cus, hipStream_t st) {
     if (nwords == 0) return hipSuccess;
     bool a16 = ((uintptr_t)dst & 15) == 0 && (nwords & 1) == 0;
@@ -107,10 +157,25 @@ hipError_t launch_or_gather(uint64_t* dst, const OrSources& s, uint64_t nwords, 
     uint64_t g = (count + 255) / 256;
     g = std::min<uint64_t>(g, (uint64_t)num_cus * 8);
     if (g < 1) g = 1;
+    if (a16) return or_gather_n((uint4*)dst, s, count, (uint32_t)g, st);
+    return or_gather_n(dst, s, count, (uint32_t)g, st);
+}
+
+// dst words of slice r (slice_words each, nwords in all) from s.p[r] where set.
+hipError_t launch_copy_slices(uint64_t* dst, const OrSources& s, uint64_t slice_words, uint64_t nwords, int num_cus,
+                              hipStream_t st) {
+    if (nwords == 0 || s.n == 0) return hipSuccess;
+    bool a16 = ((uintptr_t)dst & 15) == 0 && (nwords & 1) == 0 && (slice_words & 1) == 0;
+    for (uint32_t j = 0; j < s.n; j++) a16 = a16 && ((uintptr_t)s.p[j] & 15) == 0;
+    const uint64_t per = a16 ? slice_words / 2 : slice_words, count = a16 ? nwords / 2 : nwords;
+    uint64_t gx = (per + 1023) / 1024;  // 256 threads x 4 elements per block
+    gx = std::min<uint64_t>(gx, std::max<uint64_t>(1, (uint64_t)num_cus * 8 / s.n));
+    if (gx < 1) gx = 1;
+    const dim3 grid((uint32_t)gx, s.n);
     if (a16)
-        k_or_gather<uint4><<<dim3((uint32_t)g), dim3(256), 0, st>>>((uint4*)dst, s, count);
+        k_copy_slices<uint4><<<grid, dim3(256), 0, st>>>((uint4*)dst, s, per, count);
     else
-        k_or_gather<uint64_t><<<dim3((uint32_t)g), dim3(256), 0, st>>>(dst, s, count);
+        k_copy_slices<uint64_t><<<grid, dim3(256), 0, st>>>(dst, s, per, count);
     return hipGetLastError();
 }
 
@@ -193,26 +258,22 @@ int merge_reduce_scatter(lsmb_multi* m, uint64_t* const* part, uint64_t nw, uint
 }
 
 // All-gather of words [base, base + nw): shard g copies every other shard's
-// merged sub-slice into its words.
+// merged sub-slice into its words, all of them in one kernel of peer loads
+// (every peer link at once).
 int merge_all_gather(lsmb_multi* m, uint64_t* const* part, uint64_t nw, uint64_t base = 0, bool side = false) {
     const int G = shards(m);
+    const uint64_t per = slice_words(nw, G);
     for (int g = 0; g < G; g++) {
         lsmb_ctx* c = m->ctx[g];
         DevGuard dg(c->dev);
         const hipStream_t st = merge_stream(m, g, side);
+        OrSources s;
+        s.n = (uint32_t)G;
         for (int j = 0; j < G; j++) {
-            if (j == g) continue;
-            HIP_TRY(hipStreamWaitEvent(st, m->ev_merged[j], 0));
-            uint64_t lo, hi;
-            slice_of(nw, G, j, &lo, &hi);
-            lo += base, hi += base;
-            if (hi == lo) continue;
-            const int dj = m->ctx[j]->dev;
-            if (dj == c->dev)
-                HIP_TRY(hipMemcpyAsync(part[g] + lo, part[j] + lo, (hi - lo) * 8, hipMemcpyDeviceToDevice, st));
-            else
-                HIP_TRY(hipMemcpyPeerAsync(part[g] + lo, c->dev, part[j] + lo, dj, (hi - lo) * 8, st));
+            s.p[j] = j == g ? nullptr : part[j] + base;
+            if (j != g) HIP_TRY(hipStreamWaitEvent(st, m->ev_merged[j], 0));
         }
+        HIP_TRY(launch_copy_slices(part[g] + base, s, per, nw, c->num_cus, st));
     }
     return LSMB_OK;
 }
@@ -475,6 +536,25 @@ int lsmb_or_gather_dev(lsmb_ctx* c, void* d_dst, const void* const* d_srcs, uint
     if (((uintptr_t)d_dst & 7) != 0) return fail(LSMB_EINVAL, "d_dst is not 8-byte aligned");
     DevGuard g(c->dev);
     HIP_TRY(launch_or_gather((uint64_t*)d_dst, s, nwords, c->num_cus, pick_stream(c, stream)));
+    return LSMB_OK;
+}
+
+int lsmb_copy_slices_dev(lsmb_ctx* c, void* d_dst, const void* const* d_srcs, uint32_t nsrc, uint64_t slice_words,
+                         uint64_t nwords, void* stream) {
+    if (!c || !d_srcs) return fail(LSMB_EINVAL, "null argument");
+    if (nsrc < 1 || nsrc > (uint32_t)kMaxShards) return fail(LSMB_EINVAL, "nsrc must be in [1, %d]", kMaxShards);
+    if (nwords == 0) return LSMB_OK;
+    if (!d_dst) return fail(LSMB_EINVAL, "null device pointer");
+    if (slice_words == 0 || (slice_words * nsrc < nwords)) return fail(LSMB_EINVAL, "nsrc slices of slice_words must cover nwords");
+    OrSources s;
+    s.n = nsrc;
+    for (uint32_t j = 0; j < nsrc; j++) {
+        if (d_srcs[j] && ((uintptr_t)d_srcs[j] & 7) != 0) return fail(LSMB_EINVAL, "source %u is not 8-byte aligned", j);
+        s.p[j] = d_srcs[j];
+    }
+    if (((uintptr_t)d_dst & 7) != 0) return fail(LSMB_EINVAL, "d_dst is not 8-byte aligned");
+    DevGuard g(c->dev);
+    HIP_TRY(launch_copy_slices((uint64_t*)d_dst, s, slice_words, nwords, c->num_cus, pick_stream(c, stream)));
     return LSMB_OK;
 }
 

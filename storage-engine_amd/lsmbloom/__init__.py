@@ -111,6 +111,8 @@ SIGNATURES = {
     "lsmb_ipc_import": (ctypes.c_int, [vp, u8p, ctypes.POINTER(vp)]),
     "lsmb_ipc_close": (ctypes.c_int, [vp, vp]),
     "lsmb_or_gather_dev": (ctypes.c_int, [vp, vp, ctypes.POINTER(vp), ctypes.c_uint32, ctypes.c_uint64, vp]),
+    "lsmb_copy_slices_dev": (ctypes.c_int, [vp, vp, ctypes.POINTER(vp), ctypes.c_uint32, ctypes.c_uint64,
+                                            ctypes.c_uint64, vp]),
     "lsmb_flag_signal_dev": (ctypes.c_int, [vp, vp, ctypes.c_uint32, vp]),
     "lsmb_flag_wait_dev": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                           vp]),
@@ -387,6 +389,13 @@ class Context:
         arr = (vp * len(src_ptrs))(*[vp(int(p)) for p in src_ptrs])
         _check(lib().lsmb_or_gather_dev(self.h, vp(int(dst_ptr)), arr, len(src_ptrs), int(nwords),
                                         self._stream(stream)))
+
+    def copy_slices_dev(self, dst_ptr, src_ptrs, slice_words, nwords, stream=None):
+        """dst slice r = src_ptrs[r]'s slice r (u64 words) for every r whose source is
+        not None/0: the merge's all-gather in one kernel (lsmb_copy_slices_dev)."""
+        arr = (vp * len(src_ptrs))(*[vp(int(p or 0)) for p in src_ptrs])
+        _check(lib().lsmb_copy_slices_dev(self.h, vp(int(dst_ptr)), arr, len(src_ptrs), int(slice_words), int(nwords),
+                                          vp(stream or 0)))
 
     def flag_signal_dev(self, flag_ptr, value, stream=None):
         """After the stream's prior work: *flag = value, system-scope release (lsmb_flag_signal_dev)."""

@@ -196,7 +196,7 @@ class IpcMerge:
         if self.ordered == "host":
             self._phase_done(stream)  # every partial of the range is final
             for op in merge_schedule(self.rank, self.world, lo, hi, 0):
-                if op[0] == "gather":
+                if op[0] in ("gather", "copy"):
                     self._gather(op, stream)
                 elif op[0] == "wait" and op[1] in (1, 2):
                     self._phase_done(stream)
@@ -215,9 +215,14 @@ class IpcMerge:
         return self.words
 
     def _gather(self, op, stream):
-        _, a, b, srcs = op
-        self.ctx.or_gather_dev(self.ptrs[self.rank] + 8 * a, [self.ptrs[r] + 8 * a for r in srcs], b - a,
-                               stream=stream.cuda_stream)
+        if op[0] == "gather":
+            _, a, b, srcs = op
+            self.ctx.or_gather_dev(self.ptrs[self.rank] + 8 * a, [self.ptrs[r] + 8 * a for r in srcs], b - a,
+                                   stream=stream.cuda_stream)
+        else:  # "copy": every other rank's merged slice in one kernel
+            _, lo, hi, per, srcs = op
+            ptrs = [self.ptrs[r] + 8 * lo if r in srcs else 0 for r in range(self.world)]
+            self.ctx.copy_slices_dev(self.ptrs[self.rank] + 8 * lo, ptrs, per, hi - lo, stream=stream.cuda_stream)
 
 
 def merge_schedule(rank, world, lo, hi, epoch):
@@ -225,8 +230,11 @@ def merge_schedule(rank, world, lo, hi, epoch):
     in order: ("signal", phase, epoch) — set my flag[phase] = epoch;
     ("wait", phase, epoch) — until every rank's flag[phase] >= epoch;
     ("gather", a, b, ranks) — my words[a:b] = OR of those ranks' words[a:b]
-    (my own index among them: in place).  Phase 0: every partial of the range
-    is final; 1: every slice merged; 2: every rank holds the merged range."""
+    (my own index among them: in place); ("copy", lo, hi, per, ranks) — for
+    each listed rank r, my words of slice r (words [lo + r per, lo + (r+1) per)
+    within [lo, hi)) = rank r's (lsmb_copy_slices_dev: one kernel, every peer
+    link at once).  Phase 0: every partial of the range is final; 1: every
+    slice merged; 2: every rank holds the merged range."""
     per = _slices(hi - lo, world)
     sl = [(min(hi, lo + r * per), min(hi, lo + (r + 1) * per)) for r in range(world)]
     ops = [("signal", 0, epoch), ("wait", 0, epoch)]
@@ -234,8 +242,8 @@ def merge_schedule(rank, world, lo, hi, epoch):
     if b > a:
         ops.append(("gather", a, b, list(range(world))))
     ops += [("signal", 1, epoch), ("wait", 1, epoch)]
-    for r, (a, b) in enumerate(sl):
-        if r != rank and b > a:
-            ops.append(("gather", a, b, [r]))
+    peers = [r for r, (a, b) in enumerate(sl) if r != rank and b > a]
+    if peers:
+        ops.append(("copy", lo, hi, per, peers))
     ops += [("signal", 2, epoch), ("wait", 2, epoch)]
     return ops

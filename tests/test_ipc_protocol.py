@@ -112,8 +112,12 @@ def run(world, nwords, ranges, builds, seed, drop=None, slow_rank=None):
                                 sim.flags[me][op[1]] = op[2]
                         elif op[0] == "wait":
                             sim.wait(op[1], op[2])
-                        else:
+                        elif op[0] == "gather":
                             sim.gather(me, op[1], op[2], op[3], scale)
+                        else:  # copy: each listed rank's slice of [lo, hi) from that rank
+                            _, lo, hi, per, srcs = op
+                            for r in srcs:
+                                sim.gather(me, min(hi, lo + r * per), min(hi, lo + (r + 1) * per), [r], scale)
                 snaps[me][bi] = sim.words[me].copy()
         except Exception as ex:  # reported by the main thread
             sim.errors.append(ex)
@@ -146,11 +150,15 @@ def test_schedule_shape():
     assert kinds[:2] == ["signal", "wait"] and kinds[-2:] == ["signal", "wait"]
     assert [o[1] for o in ops if o[0] == "signal"] == [0, 1, 2]
     g = [o for o in ops if o[0] == "gather"]
-    assert g[0][1:] == (36, 62, [0, 1, 2, 3])  # my slice, all ranks' partials
-    assert all(len(o[3]) == 1 and o[3][0] != 1 for o in g[1:]) and len(g) == 4
+    assert g == [("gather", 36, 62, [0, 1, 2, 3])]  # my slice (per = 26), all ranks' partials
+    c = [o for o in ops if o[0] == "copy"]
+    assert c == [("copy", 10, 110, 26, [0, 2, 3])]  # every other rank's slice, one kernel
+    assert kinds.index("gather") < kinds.index("copy")
     assert all(o[2] == 7 for o in ops if o[0] in ("signal", "wait"))
-    covered = sorted((o[1], o[2]) for o in g)
-    assert covered[0][0] == 10 and covered[-1][1] == 110
+    # ragged: the last slice is short or empty; a rank whose slice is empty copies only
+    ops = merge_schedule(3, 4, 0, 6, 1)
+    assert [o for o in ops if o[0] == "gather"] == []
+    assert [o for o in ops if o[0] == "copy"] == [("copy", 0, 6, 2, [0, 1, 2])]
 
 
 @pytest.mark.parametrize("drop,slow", [(("wait", 2), 1), (("wait", 0), 0), (("wait", 1), 2)])

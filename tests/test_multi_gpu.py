@@ -496,3 +496,42 @@ def test_fset_and_builds_on_two_contexts_concurrently(torch, oracle):
 def a_stream(c):
     """The context's own stream (NULL selects it)."""
     return 0
+
+
+@pytest.mark.parametrize("nsrc", [1, 2, 3, 5, 8, 9, 12, 16])
+@pytest.mark.parametrize("nwords,offset", [(1 << 20, 0), (100_003, 1), (7, 0)])
+def test_or_gather_and_copy_slices_dev(torch, ctx, nsrc, nwords, offset):
+    """The merge kernels alone (lsmb_or_gather_dev: N sources at compile time
+    for N <= 8, a runtime loop above; lsmb_copy_slices_dev: every slice of a
+    range from its own source in one kernel, a NULL source leaving its slice
+    alone), against numpy; 16-B aligned and 8-B-only (offset) pointers, ragged
+    last slices, and the in-place case (the destination is source 0)."""
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device="cpu").manual_seed(nsrc * 1000 + nwords)
+    src = [torch.randint(-2 ** 62, 2 ** 62, (nwords + offset,), generator=g, dtype=torch.int64).to(dev)
+           for _ in range(nsrc)]
+    ref = _u64(src[0][offset:]).copy()
+    for s in src[1:]:
+        ref |= _u64(s[offset:])
+    dst = torch.zeros(nwords + offset, dtype=torch.int64, device=dev)
+    ctx.or_gather_dev(dst.data_ptr() + 8 * offset, [s.data_ptr() + 8 * offset for s in src], nwords)
+    torch.cuda.synchronize()
+    assert np.array_equal(_u64(dst[offset:]), ref)
+    keep = src[0].clone()  # in place: source 0 is the destination
+    ctx.or_gather_dev(src[0].data_ptr() + 8 * offset, [s.data_ptr() + 8 * offset for s in src], nwords)
+    torch.cuda.synchronize()
+    assert np.array_equal(_u64(src[0][offset:]), ref)
+    src[0].copy_(keep)
+    # copy_slices: slice r from source r, slice `skip` left alone
+    per = (nwords + nsrc - 1) // nsrc
+    per += per & 1
+    skip = nsrc // 2
+    out = torch.full((nwords + offset,), -1, dtype=torch.int64, device=dev)
+    ptrs = [s.data_ptr() + 8 * offset if r != skip else 0 for r, s in enumerate(src)]
+    ctx.copy_slices_dev(out.data_ptr() + 8 * offset, ptrs, per, nwords)
+    torch.cuda.synchronize()
+    got = _u64(out[offset:])
+    for r in range(nsrc):
+        a, b = min(nwords, r * per), min(nwords, (r + 1) * per)
+        want = np.full(b - a, np.uint64(2 ** 64 - 1)) if r == skip else _u64(src[r][offset:])[a:b]
+        assert np.array_equal(got[a:b], want), r
