@@ -677,11 +677,13 @@ def compact_line(out):
                             "roofline": _leg_roof(pr.get("roofline")),
                             "answers_equal_oracle_fixture": pr.get("answers_equal_oracle_fixture"),
                             "member_rows_all_hit": pr.get("member_rows_all_hit")}
-        for name in ("fset", "fset_mixed"):
+        for name in ("fset", "fset_mixed", "fset_rows1"):
             f = pr.get(name)
             if f:
-                legs[name] = {"ms": f["ms"], "value": f["value"], "roofline": _leg_roof(f.get("roofline")),
-                              "answers_equal_oracle_fixture": f.get("answers_equal_oracle_fixture")}
+                legs[name] = {"ms": f["ms"], "value": f["value"], "roofline": _leg_roof(f.get("roofline"))}
+                for k in ("answers_equal_oracle_fixture", "answers_equal_u64_rows"):
+                    if k in f:
+                        legs[name][k] = f[k]
     ex = out.get("c2_exact_10_bits_per_key")
     if ex:
         legs["c2_exact10"] = {k: ex.get(k) for k in ("value", "kernel_ms", "pass_a_ms", "pass_b_ms", "fill_ratio",
@@ -1172,6 +1174,7 @@ class ProbeLegs:
         self.q[: Q // 2] = self.members[self.sel]
         self.out = torch.zeros((Q, (F + 7) // 8), dtype=torch.uint8, device=dev)
         self.fout = torch.zeros(Q, dtype=torch.int64, device=dev)
+        self.fout1 = torch.zeros(Q, dtype=torch.uint8, device=dev)
         # the same F tables as a filter set, with their key ranges
         self.fs = lsmbloom.FilterSet(ctx)
         self.slots = []
@@ -1208,10 +1211,15 @@ class ProbeLegs:
     def fset_mixed(self):
         self.fsm.probe_dev(self.q, self.Q, self.fout, key_len=16)
 
+    def fset_rows1(self):  # the same set, one-byte answer rows (its 8 slots fit them)
+        self.fs.probe_dev(self.q, self.Q, self.fout1, key_len=16, row_bytes=1)
+
     def alg_bytes(self, leg):
         """Algorithmic HBM bytes of one launch: the keys, the answers and the filters."""
         if leg == "probe":
             return self.Q * 16 + self.Q * self.out.shape[1] + self.F * (12 + 8 * self.nw)
+        if leg == "fset_rows1":
+            return self.Q * 16 + self.Q + self.F * (12 + 8 * self.nw)
         return self.Q * 16 + self.Q * 8 + self.F * (12 + 8 * self.nw)
 
     def close(self):
@@ -1291,6 +1299,17 @@ def bench_probe(ctx, dev, args, world=1, rank=0, max_over_ranks=lambda x: x):
                                             "k_fset_sliced")}
     if c3fx and c3fx["Q"] == Q and c3fx["F"] == F:
         res["fset"]["answers_equal_oracle_fixture"] = _sha(P.fout) == c3fx["fset_mask_sha256"]
+    # The same set with one-byte answer rows (lsmb_fset_probe_dev_rows; its 8
+    # slots fit a byte): every row equal to the u64 row's low byte just made.
+    u64_rows = P.fout.clone()
+    r1ms = max_over_ranks(timed_ms(P.fset_rows1, args.warmup, args.steps, warm_ms=20, min_timed_ms=10))
+    res["fset_rows1"] = {"what": "lsmb_fset_probe_dev_rows: the same %d-table set, one-byte answer rows" % F,
+                         "value": round(Q * world / (r1ms * 1e-3) / 1e6, 2), "unit": "Mkeys/s", "ms": round(r1ms, 4),
+                         "algorithmic_bytes": P.alg_bytes("fset_rows1"),
+                         "answers_equal_u64_rows": bool(torch.equal(P.fout1, (u64_rows & 0xFF).to(torch.uint8))),
+                         "roofline": leg_roofline("fset_rows1" if (Q, F) == (10_000_000, 8) else None,
+                                                  P.alg_bytes("fset_rows1"), r1ms, "k_fset_sliced")}
+    del u64_rows
     mms = max_over_ranks(timed_ms(P.fset_mixed, args.warmup, args.steps, warm_ms=20, min_timed_ms=10))
     res["fset_mixed"] = {"what": "lsmb_fset_probe_dev, %d tables of two sizes: %d x new(1000, 0.01) + %d x "
                                  "new(4000, 0.01), one LDS table per size class" % (F, F // 2, F - F // 2),

@@ -431,6 +431,13 @@ int lsmb_fset_probe(lsmb_fset* fs, const uint8_t* data, const uint64_t* offsets,
 int lsmb_fset_probe_dev(lsmb_fset* fs, const void* d_data, const void* d_offsets, uint32_t key_len,
                         uint64_t n, void* d_out_mask, void* stream);
 
+/* lsmb_fset_probe_dev with answer rows of row_bytes = 1, 2, 4 or 8 bytes: row i
+ * is the u64 mask's low row_bytes bytes (LE), so a set whose live slots are
+ * all below 8 * row_bytes (e.g. 8 per-level tables in 1 byte) writes 1/8 of
+ * the u64 rows' bytes.  A live slot at or above 8 * row_bytes is LSMB_EINVAL. */
+int lsmb_fset_probe_dev_rows(lsmb_fset* fs, const void* d_data, const void* d_offsets, uint32_t key_len, uint64_t n,
+                             void* d_out, uint32_t row_bytes, void* stream);
+
 /* ---- introspection ------------------------------------------------------- */
 
 /* Name of the device build strategy the dispatcher picks for (num_bits, k, n):

@@ -50,6 +50,21 @@ __device__ __forceinline__ void store_row(uint8_t* out, uint64_t i, uint32_t str
     }
 }
 
+// A filter set's answer rows: row i = the u64 mask's low rb bytes (rb = 1, 2,
+// 4 or 8: the caller's row width, covering the highest live slot), stored
+// non-temporal (nothing in the call reads them; tools/archive/r04_out_nt.sh).
+// rb is uniform, so the width select is scalar.
+struct MaskOut {
+    uint8_t* p;
+    uint32_t rb;
+    __device__ __forceinline__ void put(uint64_t i, uint64_t o) const {
+        if (rb == 8) __builtin_nontemporal_store(o, reinterpret_cast<uint64_t*>(p) + i);
+        else if (rb == 4) __builtin_nontemporal_store((uint32_t)o, reinterpret_cast<uint32_t*>(p) + i);
+        else if (rb == 2) __builtin_nontemporal_store((uint16_t)o, reinterpret_cast<uint16_t*>(p) + i);
+        else __builtin_nontemporal_store((uint8_t)o, p + i);
+    }
+};
+
 // The bit-sliced probe's filters, passed by value in the kernel arguments:
 // the kernel reads them with scalar loads at launch instead of chasing a
 // device descriptor array, and lsmb_probe then needs no descriptor upload
@@ -367,7 +382,7 @@ __device__ __forceinline__ uint32_t key_region(const Pfx16& kx, const uint8_t* k
 // is one region lookup (key_region); descriptors staged in LDS.
 template <class Src>
 __global__ __launch_bounds__(256) void k_fset_probe(Src src, uint64_t n, const RangedFilter* __restrict__ filters,
-                                                    uint32_t nfilt, FsetRanges rg, uint64_t* __restrict__ out) {
+                                                    uint32_t nfilt, FsetRanges rg, MaskOut out) {
     __shared__ RangedFilter fl[64];
     __shared__ FsetLds L;
     for (uint32_t f = threadIdx.x; f < nfilt; f += blockDim.x) fl[f] = filters[f];
@@ -420,7 +435,7 @@ __global__ __launch_bounds__(256) void k_fset_probe(Src src, uint64_t n, const R
             }
             if (hit) m |= 1ull << R.f.out_bit;
         }
-        out[i] = m;
+        out.put(i, m);
     }
 }
 
@@ -434,7 +449,7 @@ __global__ __launch_bounds__(256) void k_fset_probe(Src src, uint64_t n, const R
 template <class Src, typename T, int K, int BS = 256, class W = Walk32>
 __global__ __launch_bounds__(BS) void k_fset_sliced(Src src, uint64_t n, const RangedFilter* __restrict__ filters,
                                                      uint32_t nfilt, FsetRanges rg, uint32_t k_,
-                                                     typename W::Mod md, uint64_t* __restrict__ out) {
+                                                     typename W::Mod md, MaskOut out) {
     // static table for the 1024-thread instantiations, as in k_probe_sliced
     extern __shared__ __align__(16) uint8_t smem_dyn[];
     __shared__ __align__(16) uint8_t smem_stat[BS == 1024 ? kProbeTableBytes : 16];
@@ -514,7 +529,7 @@ __global__ __launch_bounds__(BS) void k_fset_sliced(Src src, uint64_t n, const R
             for (uint32_t f = 0; f < nfilt; f++)
                 if ((m >> f) & 1) o |= 1ull << fl[f].f.out_bit;
         }
-        __builtin_nontemporal_store(o, &out[i]);  // (non-temporal rows: tools/archive/r04_out_nt.sh)
+        out.put(i, o);
     }
 }
 
@@ -534,7 +549,7 @@ constexpr uint32_t class_wgs_per_cu() { return std::is_same<Src, ks::Fixed16>::v
 template <class Src>
 __global__ __launch_bounds__(kClassBlock, 4 * class_wgs_per_cu<Src>()) void k_fset_classes(Src src, uint64_t n, const RangedFilter* __restrict__ filters,
                                                       uint32_t nfilt, FsetRanges rg, FsetClasses cl,
-                                                      uint64_t* __restrict__ out) {
+                                                      MaskOut out) {
     extern __shared__ __align__(16) uint8_t smem_raw[];
     __shared__ RangedFilter fl[64];
     __shared__ FsetLds L;
@@ -674,7 +689,7 @@ __global__ __launch_bounds__(kClassBlock, 4 * class_wgs_per_cu<Src>()) void k_fs
             }
             o = s;
         }
-        __builtin_nontemporal_store(o, &out[i]);  // (non-temporal rows: tools/archive/r04_out_nt.sh)
+        out.put(i, o);
     }
 }
 
@@ -691,7 +706,7 @@ uint64_t probe_wgs_per_cu(uint64_t dflt) {
 
 template <class Src>
 hipError_t fset_probe_with(const Src& src, uint64_t n, const RangedFilter* df, uint32_t nfilt, const FsetRanges& rg,
-                           const FsetClasses& cl, uint32_t shared_nb, uint32_t shared_k, uint64_t* out, int num_cus,
+                           const FsetClasses& cl, uint32_t shared_nb, uint32_t shared_k, MaskOut out, int num_cus,
                            hipStream_t st, hipEvent_t done) {
     uint64_t g = (n + 255) / 256;
     const uint64_t gmax = (uint64_t)num_cus * 8;
@@ -799,10 +814,12 @@ hipError_t probe_with(const Src& src, uint64_t n, const ProbeFilter* hf, uint32_
 }  // namespace
 
 hipError_t launch_fset_probe(const KeyBatch& kb, const RangedFilter* df, uint32_t nfilt, const FsetRanges& rg,
-                             const FsetClasses& cl, uint32_t shared_nb, uint32_t shared_k, uint64_t* out, int num_cus,
-                             hipStream_t st, hipEvent_t done) {
+                             const FsetClasses& cl, uint32_t shared_nb, uint32_t shared_k, uint8_t* out_rows,
+                             uint32_t row_bytes, int num_cus, hipStream_t st, hipEvent_t done) {
     if (kb.n == 0) return hipSuccess;
     if (nfilt > 64 || rg.npts > kFsetMaxPoints || cl.ncls > kFsetMaxClasses) return hipErrorInvalidValue;
+    if (row_bytes != 1 && row_bytes != 2 && row_bytes != 4 && row_bytes != 8) return hipErrorInvalidValue;
+    const MaskOut out{out_rows, row_bytes};
     if (kb.offsets)
         return fset_probe_with(VarLen{kb.data, kb.offsets}, kb.n, df, nfilt, rg, cl, shared_nb, shared_k, out, num_cus,
                                st, done);

@@ -1272,24 +1272,34 @@ uint64_t lsmb_fset_live_mask(const lsmb_fset* fs) {
     return m;
 }
 
-int lsmb_fset_probe_dev(lsmb_fset* fs, const void* d_data, const void* d_offsets, uint32_t key_len, uint64_t n,
-                        void* d_out, void* stream) {
+int lsmb_fset_probe_dev_rows(lsmb_fset* fs, const void* d_data, const void* d_offsets, uint32_t key_len, uint64_t n,
+                             void* d_out, uint32_t row_bytes, void* stream) {
     if (!fs) return fail(LSMB_EINVAL, "null filter set");
+    if (row_bytes != 1 && row_bytes != 2 && row_bytes != 4 && row_bytes != 8)
+        return fail(LSMB_EINVAL, "row_bytes must be 1, 2, 4 or 8");
+    const uint64_t live = lsmb_fset_live_mask(fs);
+    if (row_bytes < 8 && (live >> (8 * row_bytes)) != 0)
+        return fail(LSMB_EINVAL, "a live slot does not fit %u-byte rows", row_bytes);
     if (n == 0) return LSMB_OK;
     if (!d_out || !d_data) return fail(LSMB_EINVAL, "null keys or output");
     DevGuard g(fs->c->dev);
     if (int rc = fset_refresh(fs)) return rc;
     const hipStream_t st = pick_stream(fs->c, stream);
     if (fs->ndesc == 0) {
-        HIP_TRY(hipMemsetAsync(d_out, 0, n * 8, st));
+        HIP_TRY(hipMemsetAsync(d_out, 0, n * row_bytes, st));
         return LSMB_OK;
     }
     KeyBatch kb{(const uint8_t*)d_data, (const uint64_t*)d_offsets, key_len, n};
     hipEvent_t ev;
     if (int rc = fset_probe_event(fs, st, &ev)) return rc;
     HIP_TRY(launch_fset_probe(kb, (const RangedFilter*)fs->desc.p, fs->ndesc, fs->rg, fs->cl, fs->shared_nb, fs->shared_k,
-                              (uint64_t*)d_out, fs->c->num_cus, st, ev));
+                              (uint8_t*)d_out, row_bytes, fs->c->num_cus, st, ev));
     return LSMB_OK;
+}
+
+int lsmb_fset_probe_dev(lsmb_fset* fs, const void* d_data, const void* d_offsets, uint32_t key_len, uint64_t n,
+                        void* d_out, void* stream) {
+    return lsmb_fset_probe_dev_rows(fs, d_data, d_offsets, key_len, n, d_out, 8, stream);
 }
 
 int lsmb_fset_probe(lsmb_fset* fs, const uint8_t* data, const uint64_t* offsets, uint32_t key_len, uint64_t n,
@@ -1311,7 +1321,7 @@ int lsmb_fset_probe(lsmb_fset* fs, const uint8_t* data, const uint64_t* offsets,
     hipEvent_t ev;
     if (int rc = fset_probe_event(fs, c->st, &ev)) return rc;
     HIP_TRY(launch_fset_probe(kb, (const RangedFilter*)fs->desc.p, fs->ndesc, fs->rg, fs->cl, fs->shared_nb, fs->shared_k,
-                              (uint64_t*)c->out.p, c->num_cus, c->st, ev));
+                              (uint8_t*)c->out.p, 8, c->num_cus, c->st, ev));
     HIP_TRY(hipMemcpyAsync(out_mask, c->out.p, n * 8, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(hipStreamSynchronize(c->st));
     return LSMB_OK;

@@ -187,8 +187,8 @@ struct FsetClasses {
 // entry width; several classes the per-class tables; none the L2 walk.
 // done (optional): an event the dispatch itself completes (see launch_done).
 hipError_t launch_fset_probe(const KeyBatch& kb, const RangedFilter* d_filters, uint32_t nfilt, const FsetRanges& rg,
-                             const FsetClasses& cl, uint32_t shared_nb, uint32_t shared_k, uint64_t* d_out,
-                             int num_cus, hipStream_t st, hipEvent_t done = nullptr);
+                             const FsetClasses& cl, uint32_t shared_nb, uint32_t shared_k, uint8_t* d_out_rows,
+                             uint32_t row_bytes, int num_cus, hipStream_t st, hipEvent_t done = nullptr);
 
 // A kernel launch whose completion also completes `done` (when non-null):
 // hipExtLaunchKernelGGL tracks the event with the dispatch's own completion

@@ -89,6 +89,7 @@ SIGNATURES = {
     "lsmb_fset_live_mask": (ctypes.c_uint64, [vp]),
     "lsmb_fset_probe": (ctypes.c_int, [vp, u8p, u64p, ctypes.c_uint32, ctypes.c_uint64, u64p]),
     "lsmb_fset_probe_dev": (ctypes.c_int, [vp, vp, vp, ctypes.c_uint32, ctypes.c_uint64, vp, vp]),
+    "lsmb_fset_probe_dev_rows": (ctypes.c_int, [vp, vp, vp, ctypes.c_uint32, ctypes.c_uint64, vp, ctypes.c_uint32, vp]),
     "lsmb_build_strategy": (ctypes.c_char_p, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]),
     "lsmb_host_max_keys": (ctypes.c_uint64, []),
     "lsmb_build_sweeps": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]),
@@ -588,10 +589,17 @@ class FilterSet:
         np.cumsum(lens, out=offs[1:])
         return self.probe(np.frombuffer(b"".join(bytes(k) for k in keys), dtype=np.uint8), offs)
 
-    def probe_dev(self, data, n, out, offsets=None, key_len=0, stream=None):
-        _check(lib().lsmb_fset_probe_dev(self.h, vp(data.data_ptr()),
-                                         vp(offsets.data_ptr()) if offsets is not None else None, key_len, n,
-                                         vp(out.data_ptr()), Context._stream(stream)))
+    def probe_dev(self, data, n, out, offsets=None, key_len=0, stream=None, row_bytes=8):
+        """Device keys -> device answer rows: u64 per key (lsmb_fset_probe_dev),
+        or row_bytes = 1 / 2 / 4 per key when every live slot fits them
+        (lsmb_fset_probe_dev_rows)."""
+        offs = vp(offsets.data_ptr()) if offsets is not None else None
+        if row_bytes == 8:
+            _check(lib().lsmb_fset_probe_dev(self.h, vp(data.data_ptr()), offs, key_len, n, vp(out.data_ptr()),
+                                             Context._stream(stream)))
+        else:
+            _check(lib().lsmb_fset_probe_dev_rows(self.h, vp(data.data_ptr()), offs, key_len, n, vp(out.data_ptr()),
+                                                  int(row_bytes), Context._stream(stream)))
 
 
 def build_strategy(num_bits, n, k=7):

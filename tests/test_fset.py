@@ -416,3 +416,44 @@ def test_fset_mixed_size_classes_varlen_keys(oracle):
     assert [int(x) for x in got] == expected_masks(oracle, tables, q)
     fs.close()
     ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sizes", [(1000,) * 8, (1000, 4000) * 4, (1000,) * 5 + (10 ** 9,), (1000,) * 12])
+def test_fset_compact_rows(oracle, sizes):
+    """lsmb_fset_probe_dev_rows: answer rows of 1, 2 or 4 bytes are the u64
+    rows' low bytes on every kernel path (same-size sliced table, size
+    classes, the generic L2 walk next to a saturated filter), and a live slot
+    that does not fit the row width is LSMB_EINVAL."""
+    import torch
+
+    ctx = lsmbloom.Context(0)
+    fs = FilterSet(ctx)
+    for t, m in enumerate(sizes):
+        nk = min(m, 3000)
+        keys = keygen.key16(0x5EED0400 + t, 0, nk)
+        rows = sorted(bytes(r) for r in keys)
+        nb, k = lsmbloom.params(m, 0.01)
+        fs.add_filter(BloomFilter(oracle.build_fixed(keys, 16, nb, k), k, nb), rows[nk // 5], rows[4 * nk // 5])
+    q = np.concatenate([keygen.key16(0x5EED0400 + t, 0, 2000) for t in range(len(sizes))]
+                       + [keygen.key16(0x5EED0500, 0, 30_000)])
+    n = q.shape[0]
+    dq = torch.from_numpy(np.ascontiguousarray(q)).to("cuda:0")
+    full = torch.zeros(n, dtype=torch.int64, device="cuda:0")
+    fs.probe_dev(dq, n, full, key_len=16)
+    torch.cuda.synchronize()
+    ref = full.cpu().numpy().view(np.uint64)
+    assert ref.any()
+    for rb, dt in ((1, np.uint8), (2, np.uint16), (4, np.uint32)):
+        out = torch.full((n * rb,), 0xA5, dtype=torch.uint8, device="cuda:0")
+        if len(sizes) > 8 * rb:
+            with pytest.raises(lsmbloom.LsmbError) as ei:
+                fs.probe_dev(dq, n, out, key_len=16, row_bytes=rb)
+            assert ei.value.code == lsmbloom.LSMB_EINVAL
+            continue
+        fs.probe_dev(dq, n, out, key_len=16, row_bytes=rb)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(dt)
+        assert np.array_equal(got, ref.astype(dt)), rb
+    fs.close()
+    ctx.close()

@@ -11,6 +11,7 @@ kernels after the setup, so a pass's per-kernel means belong to this leg.
   probe     C3: 10 M keys x 8 new(1000, 0.01) filters, lsmb_probe_dev
   fset      the same through the device filter set (range pre-check + bloom)
   fset_mixed  a filter set of two sizes (4 x new(1000) + 4 x new(4000))
+  fset_rows1  the fset leg with one-byte answer rows (lsmb_fset_probe_dev_rows)
 """
 import argparse
 import os
@@ -23,7 +24,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 import bench  # noqa: E402  (the legs' shared setup: ProbeLegs, seeds)
 
-LEGS = ("c2", "exact10", "c5", "c4", "probe", "fset", "fset_mixed")
+LEGS = ("c2", "exact10", "c5", "c4", "probe", "fset", "fset_mixed", "fset_rows1")
 
 
 def main():

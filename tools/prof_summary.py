@@ -117,6 +117,7 @@ LEG_KERNELS = {
     "probe": ("k_probe_sliced",),
     "fset": ("k_fset_sliced",),
     "fset_mixed": ("k_fset_classes",),
+    "fset_rows1": ("k_fset_sliced",),
 }
 LEG_REPS = 10
 COUNTERS = {"FETCH_SIZE": "read_bytes", "WRITE_SIZE": "write_bytes", "SQ_INSTS_VALU": "valu_insts",
