@@ -447,9 +447,8 @@ def test_fset_compact_rows(oracle, sizes):
     for rb, dt in ((1, np.uint8), (2, np.uint16), (4, np.uint32)):
         out = torch.full((n * rb,), 0xA5, dtype=torch.uint8, device="cuda:0")
         if len(sizes) > 8 * rb:
-            with pytest.raises(lsmbloom.LsmbError) as ei:
+            with pytest.raises(ValueError, match="does not fit"):  # LSMB_EINVAL, as the mirror raises it
                 fs.probe_dev(dq, n, out, key_len=16, row_bytes=rb)
-            assert ei.value.code == lsmbloom.LSMB_EINVAL
             continue
         fs.probe_dev(dq, n, out, key_len=16, row_bytes=rb)
         torch.cuda.synchronize()
