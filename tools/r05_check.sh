@@ -1,6 +1,6 @@
 #!/bin/bash
 # One GPU call: the whole -m gpu suite, smoke(), then the default bench line
-# (the driver's command).  Stops at the first step that fails.
+# (the driver's command: no flags).  Stops at the first step that fails.
 # Usage: tools/r05_check.sh <tag>
 TAG=${1:-r05chk}
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -11,7 +11,7 @@ tail -3 gpurun_out/${TAG}_tests.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || exit $?
 tail -1 gpurun_out/${TAG}_smoke.log
-timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err
+timeout -k 10 300 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err
 brc=$?
 echo "bench rc=$brc"
 exit $brc
