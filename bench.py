@@ -58,6 +58,7 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory end-to-end measurement")
     ap.add_argument("--no-varlen", action="store_true", help="skip the C4 variable-length build leg")
     ap.add_argument("--no-exact10", action="store_true", help="skip the C2 exact 10 bits/key leg")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 shard leg (N = 1)")
     ap.add_argument("--no-c1", action="store_true", help="skip the C1-on-the-GPU leg")
     ap.add_argument("--no-overlap", action="store_true",
                     help="N > 1: build the whole filter, then OR-allreduce it (no per-sweep overlap)")
@@ -579,6 +580,9 @@ def main():
     torch.cuda.empty_cache()
     if not args.no_varlen and world == 1:
         out["varlen"] = bench_varlen(ctx, dev, args)
+    if not args.no_c5 and world == 1:
+        out["c5_shard"] = bench_c5_shard(ctx, dev)
+        torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(nb, k, args.cpu_seconds)
         out["cpu_baseline"]["gpu_over_cpu_1thread"] = round(value / out["cpu_baseline"]["value"], 1)
@@ -694,6 +698,11 @@ def compact_line(out):
         legs["c4"] = {k: vl.get(k) for k in ("value", "ms_per_step", "kernel_ms", "pass_a_ms", "pass_b_ms",
                                              "words_equal_oracle_fixture")}
         legs["c4"]["roofline"] = _leg_roof(vl.get("roofline"))
+    c5 = out.get("c5_shard")
+    if c5:
+        legs["c5_shard"] = {k: c5.get(k) for k in ("value", "kernel_ms", "pass_a_ms", "pass_b_ms",
+                                                   "words_equal_oracle_fixture")}
+        legs["c5_shard"]["roofline"] = _leg_roof(c5.get("roofline"))
     c1 = out.get("c1_gpu")
     if c1:
         legs["c1_gpu"] = {"build_ms": c1["build"]["ms"], "probe_ms": c1["probe"]["ms"],
@@ -828,6 +837,41 @@ def bench_exact10(ctx, keys, n, reps=10):
     if n == 100_000_000:
         res["words_equal_oracle_fixture"] = fixture_check(w, "c2_exact10", nb)
     del w
+    return res
+
+
+def bench_c5_shard(ctx, dev, reps=10):
+    """configs[4]'s per-GPU build on one GPU: the first 125 M C5 keys (shard 0
+    of 8) into new(1e9, 0.01) = 2^32-1 bits, fresh, device-resident keys
+    generated on the device; every word against the oracle's digest
+    (tests/golden/fullsize_fixture.json "c5_shard0")."""
+    import numpy as np
+    import torch
+
+    import lsmbloom
+    n = 125_000_000
+    nb, k = lsmbloom.params(1_000_000_000, 0.01)
+    keys = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+    ctx.gen_key16_dev(SEED_MEMBERS, 0, n, keys)
+    w = torch.empty(lsmbloom.num_words(nb), dtype=torch.int64, device=dev)
+    ctx.set_timing(True)
+    kt = np.zeros(3)
+    for i in range(reps + 2):
+        ctx.build_fixed_dev_new(keys, 16, n, nb, k, w)
+        ctx.sync()
+        torch.cuda.synchronize(dev)
+        if i >= 2:
+            kt += np.array(ctx.last_build_ms())
+    ctx.set_timing(False)
+    kt /= reps
+    alg = 16 * n + 8 * lsmbloom.num_words(nb)
+    res = {"workload": "C5 shard 0 of 8: %d 16-B keys into new(1e9, 0.01) = %d bits, k = %d" % (n, nb, k),
+           "value": round(n / (kt[0] * 1e-3) / 1e6, 1), "unit": "Mkeys/s", "kernel_ms": round(float(kt[0]), 4),
+           "pass_a_ms": round(float(kt[1]), 4), "pass_b_ms": round(float(kt[2]), 4),
+           "strategy": lsmbloom.build_strategy(nb, n, k),
+           "roofline": leg_roofline("c5", alg, kt[0], "build (2 sweeps of k_bin + k_apply<21> + k_ovf_apply)")}
+    res["words_equal_oracle_fixture"] = fixture_check(w, "c5_shard0", nb)
+    del w, keys
     return res
 
 

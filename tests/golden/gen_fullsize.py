@@ -10,7 +10,8 @@ first/last 8 words.  tests/test_gpu_parity.py and bench.py compare the GPU's
 full-size filters against these digests, so full-size parity no longer needs
 the oracle at run time.
 
-Run here (CPU): python3 tests/golden/gen_fullsize.py  (~2-4 min, ~3 GB RAM)
+Run here (CPU): python3 tests/golden/gen_fullsize.py  (~2-4 min, ~3 GB RAM);
+`gen_fullsize.py c5_shard0` adds or refreshes that entry alone.
 """
 import hashlib
 import json
@@ -54,8 +55,23 @@ def build_c4(orc, n, nb, k, chunk=10_000_000):
     return words
 
 
+def c5_shard0(orc):
+    """The N = 8 per-GPU C5 build on one GPU (bench.py's c5_shard leg): the
+    first 125 M C5 keys into new(1e9, 0.01) = 2^32-1 bits."""
+    nb5, k5 = orc.params(1_000_000_000, 0.01)
+    return digest(build_key16(orc, 125_000_000, nb5, k5), nb5, k5,
+                  "C5 shard 0 of 8: key16(0x5EED0001, 0..1.25e8) into new(1e9, 0.01) = 2^32-1 bits")
+
+
 def main():
     orc = oracle_ct.load()
+    path = os.path.join(HERE, "fullsize_fixture.json")
+    if sys.argv[1:] == ["c5_shard0"]:  # add / refresh that entry only (~1 min)
+        out = json.load(open(path))
+        out["c5_shard0"] = c5_shard0(orc)
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+        return
     out = {}
     t0 = time.time()
     nb, k = orc.params(100_000_000, 0.01)
@@ -72,7 +88,8 @@ def main():
     out["c5"] = digest(build_key16(orc, 1_000_000_000, nb5, k5), nb5, k5,
                        "C5: key16(0x5EED0001, 0..1e9) into new(1e9, 0.01) = 2^32-1 bits")
     print("c5 %.0fs" % (time.time() - t0), flush=True)
-    with open(os.path.join(HERE, "fullsize_fixture.json"), "w") as f:
+    out["c5_shard0"] = c5_shard0(orc)
+    with open(path, "w") as f:
         json.dump(out, f, indent=1)
 
 

@@ -53,9 +53,10 @@ def test_compact_line_fits_the_driver_tail():
     """VERDICT r04 "missing" item 2: the driver keeps ~8 KB of output, so the
     one JSON line must carry every leg (the C3 probe half of the metric
     included) within LINE_BUDGET bytes.  Checked on the committed full record
-    of a round-4 run (profiles/r04/r04h_bench.json, all legs present)."""
+    of a round-5 run (profiles/r05/r05r_bench_detail.json, every leg present,
+    the C5 shard and the one-byte filter-set rows included)."""
     import json
-    full = json.loads(open(os.path.join(ROOT, "profiles", "r04", "r04h_bench.json")).read())
+    full = json.loads(open(os.path.join(ROOT, "profiles", "r05", "r05r_bench_detail.json")).read())
     full["detail"] = "gpurun_out/bench_detail.json"
     line = json.dumps(bench.compact_line(full), separators=(",", ":"))
     assert len(line) < bench.LINE_BUDGET
@@ -67,6 +68,8 @@ def test_compact_line_fits_the_driver_tail():
         assert k in c["roofline"], k
     for k in ("value", "unit", "cores", "kind", "sample"):
         assert k in c["cpu_baseline"], k
-    assert set(c["legs"]) >= {"c3_probe", "fset", "fset_mixed", "c2_exact10", "c4", "c1_gpu", "e2e"}
+    assert set(c["legs"]) >= {"c3_probe", "fset", "fset_mixed", "fset_rows1", "c2_exact10", "c4", "c5_shard",
+                              "c1_gpu", "e2e"}
+    assert c["legs"]["c5_shard"]["words_equal_oracle_fixture"] is True
     assert c["legs"]["c3_probe"]["ms"] == full["probe"]["ms"]
     assert c["legs"]["c3_probe"]["answers_equal_oracle_fixture"] is True

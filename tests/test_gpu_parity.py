@@ -474,6 +474,28 @@ def test_c2_exact10_full_size_fixture(ctx):
     assert_full_fixture(words.cpu().numpy().view(np.uint64), "c2_exact10")
 
 
+@pytest.mark.parametrize("fresh", [True, False])
+def test_c5_shard0_fixture(ctx, fresh):
+    """configs[4]'s per-GPU build: the first 125 M C5 keys (shard 0 of 8) into
+    new(1e9, 0.01) = 2^32-1 bits (two sweeps of 2^21-bit bins), fresh and
+    OR-accumulate into zeros, every word against the oracle's digest."""
+    import torch
+    n = 125_000_000
+    nb, k = lsmbloom.params(1_000_000_000, 0.01)
+    dev = torch.device("cuda:0")
+    keys = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+    ctx.gen_key16_dev(0x5EED0001, 0, n, keys)
+    if fresh:
+        words = torch.full((lsmbloom.num_words(nb),), -1, dtype=torch.int64, device=dev)  # garbage: output-only
+        ctx.build_fixed_dev_new(keys, 16, n, nb, k, words)
+    else:
+        words = torch.zeros(lsmbloom.num_words(nb), dtype=torch.int64, device=dev)
+        ctx.build_fixed_dev(keys, 16, n, nb, k, words)
+    torch.cuda.synchronize()
+    del keys
+    assert_full_fixture(words.cpu().numpy().view(np.uint64), "c5_shard0")
+
+
 def test_c5_full_size_shards_or_equal_monolithic(ctx):
     """C5 data path at full size on one GPU: 1e9 16-B keys, filter new(1e9, 0.01)
     (2^32-1 bits, 512 MiB).  Eight shard builds (one per would-be rank) merged
