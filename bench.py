@@ -394,15 +394,23 @@ def main():
         # The merges must agree word for word (one serial step each, untimed,
         # before any warm-up) and the IPC merge's waits must all have been
         # met; otherwise only RCCL is timed.
-        snaps = {}
+        snaps, failed = {}, None
         for f in merges:
-            step(False, f)
+            try:
+                step(False, f)
+                torch.cuda.synchronize(dev)
+            except Exception as e:  # an IPC merge error drops IPC (its waits time out on the peers)
+                if f != "ipc":
+                    raise
+                failed = repr(e)[:200]
             barrier()
             snaps[f] = words.clone()
         names = list(snaps)
-        agree = all(torch.equal(snaps[names[0]], snaps[x]) for x in names[1:])
+        agree = failed is None and all(torch.equal(snaps[names[0]], snaps[x]) for x in names[1:])
         del snaps
-        if ipc is not None and ipc.timeouts():
+        if failed:
+            merge_notes["ipc_error"] = failed
+        elif ipc is not None and ipc.timeouts():
             agree = False
             merge_notes["ipc_error"] = "flag waits timed out in the agreement step"
         t = torch.tensor([1 if agree else 0], dtype=torch.int32, device=dev if not host_coll else "cpu")
