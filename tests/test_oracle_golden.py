@@ -156,3 +156,24 @@ def test_deserialize_validation(oracle):
         oracle.deserialize(ser + b"extra")
     k2, nb2, w2 = oracle.deserialize(ser)
     assert (k2, nb2) == (k, nb) and np.array_equal(w, w2)
+
+
+def test_fullsize_fixture_fill_ratios(oracle):
+    """The full-size digests (tests/golden/gen_fullsize.py) are plausible Bloom
+    filters of their stated workloads: sizing as BloomFilter::new gives it,
+    and the fill ratio within 1e-4 of 1 - exp(-k n / m) (its standard
+    deviation here is ~1e-5)."""
+    import math
+    fx = json.load(open(os.path.join(GOLD, "fullsize_fixture.json")))
+    work = {"c2": (10**8, 10**8), "c2_exact10": (10**8, None), "c4": (10**8, 10**8),
+            "c5": (10**9, 10**9), "c5_shard0": (125_000_000, 10**9)}
+    assert set(fx) == set(work)
+    for name, (n, sized_for) in work.items():
+        e = fx[name]
+        if sized_for is None:
+            assert (e["num_bits"], e["k"]) == (10 * n, 7)
+        else:
+            assert (e["num_bits"], e["k"]) == tuple(oracle.params(sized_for, 0.01)), name
+        assert e["words"] == (e["num_bits"] + 63) // 64
+        want = 1.0 - math.exp(-e["k"] * n / e["num_bits"])
+        assert abs(e["popcount"] / e["num_bits"] - want) < 1e-4, name
