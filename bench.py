@@ -46,7 +46,12 @@ def parse():
     ap.add_argument("--backend", default="auto",
                     help="N>1 merge: auto (RCCL and IPC both set up; the untimed calibration checks that they agree "
                          "word for word and times the faster), nccl (RCCL collectives only), gloo (host-staged), "
-                         "ipc (peer loads over IPC-mapped device words, device-ordered phases)")
+                         "ipc (peer loads over IPC-mapped device words, device-ordered phases), auto-gloo (auto "
+                         "with gloo in RCCL's place).  nccl and auto need one GPU per rank")
+    ap.add_argument("--allow-shared-gpu", action="store_true",
+                    help="let auto run with more ranks than visible GPUs (as ipc: a one-GPU rehearsal; the line then "
+                         "says ranks_per_gpu > 1 and is not a scaling figure)")
+    ap.add_argument("--inject-merge-fault", action="store_true", help=argparse.SUPPRESS)  # tests: a wrong merge
     ap.add_argument("--probe-keys", type=int, default=10_000_000)
     ap.add_argument("--probe-filters", type=int, default=8)
     ap.add_argument("--no-probe", action="store_true")
@@ -59,6 +64,8 @@ def parse():
     ap.add_argument("--no-varlen", action="store_true", help="skip the C4 variable-length build leg")
     ap.add_argument("--no-exact10", action="store_true", help="skip the C2 exact 10 bits/key leg")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 shard leg (N = 1)")
+    ap.add_argument("--no-c5-full", action="store_true",
+                    help="skip the C5 full leg (N = 1: all 1e9 C5 keys on one GPU, the N > 1 curve's 1-GPU point)")
     ap.add_argument("--no-c1", action="store_true", help="skip the C1-on-the-GPU leg")
     ap.add_argument("--no-overlap", action="store_true",
                     help="N > 1: build the whole filter, then OR-allreduce it (no per-sweep overlap)")
@@ -255,8 +262,11 @@ def main():
     ndev = torch.cuda.device_count()
     backend = args.backend
     if world > 1 and backend in ("nccl", "auto") and world > ndev:
-        if backend == "nccl":
-            print("bench.py: %d RCCL ranks need %d GPUs, %d visible" % (world, world, ndev), file=sys.stderr)
+        if backend == "nccl" or not args.allow_shared_gpu:
+            # a misconfigured HIP_VISIBLE_DEVICES must not produce an "N-GPU"
+            # line measured on fewer GPUs
+            print("bench.py: %d ranks need %d GPUs for --backend %s, %d visible (--allow-shared-gpu, --backend ipc "
+                  "or auto-gloo run ranks sharing a GPU)" % (world, world, backend, ndev), file=sys.stderr)
             sys.exit(2)
         backend = "ipc"  # ranks sharing a GPU (one-GPU rehearsal): RCCL refuses them, IPC does not
     dev = torch.device("cuda", local % max(1, ndev))
@@ -329,7 +339,7 @@ def main():
         if backend in ("ipc", "auto", "auto-gloo"):
             err = None
             try:
-                ipc = ldist.IpcMerge(words, ctx, group=side_group)
+                ipc = ldist.IpcMerge(words, ctx, group=side_group, ordered="device")
             except Exception as e:  # e.g. no IPC mapping between these GPUs: keep RCCL
                 err = repr(e)[:200]
             ok = torch.tensor([0 if err else 1], dtype=torch.int32)
@@ -410,9 +420,9 @@ def main():
         del snaps
         if failed:
             merge_notes["ipc_error"] = failed
-        elif ipc is not None and ipc.timeouts():
+        elif ipc is not None and ipc.status()[0]:
             agree = False
-            merge_notes["ipc_error"] = "flag waits timed out in the agreement step"
+            merge_notes["ipc_error"] = "merge poisoned in the agreement step (%d flag waits timed out)" % ipc.timeouts()
         t = torch.tensor([1 if agree else 0], dtype=torch.int32, device=dev if not host_coll else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         merge_notes["merges_agree"] = bool(t.item())
@@ -509,6 +519,8 @@ def main():
     if world > 1:
         moved = 2 * (world - 1) / world * 8 * nw
         out["config"]["backend"] = backend
+        out["config"]["physical_gpus"] = min(world, ndev)
+        out["config"]["ranks_per_gpu"] = -(-world // max(1, ndev))
         merge_what = {"ipc": "ipc: peer loads over IPC-mapped words (OR gather reduce-scatter + copy all-gather), "
                              "phases ordered by device flags",
                       "rccl": "rccl: all_to_all reduce-scatter + native OR kernel + all_gather",
@@ -531,6 +543,8 @@ def main():
         # workload (C5 on one GPU), for the strong-scaling curve.
         step()
         torch.cuda.synchronize(dev)
+        if args.inject_merge_fault and rank == 0:
+            words[nw // 3] ^= 1 << 17  # tests: a merge that lost a bit must invalidate the line
         if rank == 0:
             try:
                 ref = torch.zeros_like(words)
@@ -555,8 +569,12 @@ def main():
                 out["multi_gpu_check_error"] = repr(e)[:200]
         if ipc:
             torch.cuda.synchronize(dev)
-            out["step_split"]["flag_timeouts"] = int(max_over_ranks(float(ipc.timeouts())))
+            poisoned, tmo = ipc.status()
+            out["step_split"]["flag_timeouts"] = int(max_over_ranks(float(tmo)))
+            out["step_split"]["merge_poisoned"] = bool(max_over_ranks(float(poisoned)))
         out["step_split"].update(merge_notes)
+        if "single_gpu_same_workload" in out:
+            out["speedup_vs_single_gpu_same_workload"] = round(out["single_gpu_same_workload"]["ms"] / ms, 3)
         dist.barrier()
 
     # Full-size parity in the bench line itself: the filter the timed steps built
@@ -567,6 +585,17 @@ def main():
         if name:
             torch.cuda.synchronize(dev)
             out["words_equal_oracle_fixture"] = fixture_check(words, name, nb)
+    # A line whose own checks fail publishes no number:
+    # value null, the reasons listed, and a non-zero exit after the line.
+    invalid = invalid_reasons(out, timed_merge=form if world > 1 else None)
+    if world > 1:  # every rank exits the same way
+        bad = torch.tensor([1 if invalid else 0], dtype=torch.int32, device="cpu" if host_coll else dev)
+        dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+        if int(bad.item()) and not invalid:
+            invalid = ["a check failed on another rank"]
+    if invalid:
+        out["value"] = None
+        out["invalid"] = invalid
     if args.verify and rank == 0 and world == 1:
         import oracle_ct
         orc = oracle_ct.load()
@@ -591,6 +620,9 @@ def main():
     if not args.no_c5 and world == 1:
         out["c5_shard"] = bench_c5_shard(ctx, dev)
         torch.cuda.empty_cache()
+    if not args.no_c5_full and world == 1:
+        out["c5_full"] = bench_c5_full(ctx, dev)
+        torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(nb, k, args.cpu_seconds)
         out["cpu_baseline"]["gpu_over_cpu_1thread"] = round(value / out["cpu_baseline"]["value"], 1)
@@ -602,10 +634,28 @@ def main():
         out["detail"] = write_detail(out, args.detail_out)
         print(json.dumps(compact_line(out), separators=(",", ":")), flush=True)
     if ipc:
-        ipc.close(check=False)  # (timeouts, if any, are in step_split.flag_timeouts)
+        ipc.close(check=False)  # (a poisoned merge is in step_split and `invalid`)
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+    if out.get("invalid"):
+        sys.exit(3)
+
+
+def invalid_reasons(out, timed_merge=None):
+    """Why this line's headline number cannot stand: a failed word check, an
+    error in the self-check, or (N > 1, the timed merge IPC) a poisoned merge
+    or a flag wait that timed out during the timed steps."""
+    why = []
+    for k in ("words_equal_oracle_fixture", "multi_gpu_merged_equals_single_gpu_build", "verified_bit_exact"):
+        if out.get(k) is False:
+            why.append(k + " is false")
+    if out.get("multi_gpu_check_error"):
+        why.append("multi_gpu_check_error")
+    ss = out.get("step_split") or {}
+    if timed_merge == "ipc" and (ss.get("flag_timeouts") or ss.get("merge_poisoned")):
+        why.append("the timed IPC merge was poisoned (%s flag waits timed out)" % ss.get("flag_timeouts"))
+    return why
 
 
 def write_detail(out, path):
@@ -669,8 +719,8 @@ def compact_line(out):
         if "phase" in hw:
             r["pass_a_phase"] = {k: v for k, v in hw["phase"].items() if k != "source"}
     c["roofline"] = r
-    for k in ("words_equal_oracle_fixture", "multi_gpu_merged_equals_single_gpu_build", "multi_gpu_check_error",
-              "verified_bit_exact"):
+    for k in ("invalid", "words_equal_oracle_fixture", "multi_gpu_merged_equals_single_gpu_build",
+              "multi_gpu_check_error", "verified_bit_exact", "speedup_vs_single_gpu_same_workload"):
         if k in out:
             c[k] = out[k]
     if "step_split" in out:
@@ -678,7 +728,7 @@ def compact_line(out):
         c["step_split"] = {k: ss.get(k) for k in ("build_ms", "or_allreduce_ms", "serial_ms_per_step",
                                                   "or_allreduce_bytes_per_gpu", "or_allreduce_GBs_per_gpu",
                                                   "overlap_calibration", "timed_step", "merge", "merges_available",
-                                                  "merges_agree", "ipc_error", "flag_timeouts")}
+                                                  "merges_agree", "ipc_error", "flag_timeouts", "merge_poisoned")}
     if "single_gpu_same_workload" in out:
         sg = out["single_gpu_same_workload"]
         c["single_gpu_same_workload"] = {"ms": sg.get("ms"), "value": sg.get("value")}
@@ -711,6 +761,10 @@ def compact_line(out):
         legs["c5_shard"] = {k: c5.get(k) for k in ("value", "kernel_ms", "pass_a_ms", "pass_b_ms",
                                                    "words_equal_oracle_fixture")}
         legs["c5_shard"]["roofline"] = _leg_roof(c5.get("roofline"))
+    c5f = out.get("c5_full")
+    if c5f:
+        legs["c5_full"] = {k: c5f.get(k) for k in ("value", "ms", "kernel_ms", "sweeps", "words_equal_oracle_fixture")}
+        legs["c5_full"]["roofline"] = _leg_roof(c5f.get("roofline"))
     c1 = out.get("c1_gpu")
     if c1:
         legs["c1_gpu"] = {"build_ms": c1["build"]["ms"], "probe_ms": c1["probe"]["ms"],
@@ -879,6 +933,47 @@ def bench_c5_shard(ctx, dev, reps=10):
            "strategy": lsmbloom.build_strategy(nb, n, k),
            "roofline": leg_roofline("c5", alg, kt[0], "build (2 sweeps of k_bin + k_apply<21> + k_ovf_apply)")}
     res["words_equal_oracle_fixture"] = fixture_check(w, "c5_shard0", nb)
+    del w, keys
+    return res
+
+
+def bench_c5_full(ctx, dev, reps=4):
+    """configs[4]'s whole run on ONE GPU: all 1e9 C5 keys into new(1e9, 0.01) =
+    2^32-1 bits, built the way each rank builds its shard at N > 1 (fresh,
+    sweep by sweep: lsmb_build_fixed_dev_sweep_new), device-resident keys
+    generated on the device, every word against the oracle's digest
+    (tests/golden/fullsize_fixture.json "c5").  The 1-GPU point of the N > 1
+    strong-scaling curve, whose lines time the same workload split N ways."""
+    import numpy as np
+    import torch
+
+    import lsmbloom
+    n = 1_000_000_000
+    nb, k = lsmbloom.params(n, 0.01)
+    keys = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+    ctx.gen_key16_dev(SEED_MEMBERS, 0, n, keys)
+    w = torch.empty(lsmbloom.num_words(nb), dtype=torch.int64, device=dev)
+    nsw = lsmbloom.build_sweeps(nb, n, k)
+
+    def build():
+        for s in range(nsw):
+            ctx.build_fixed_dev_sweep_new(keys, 16, n, nb, k, w, s)
+    build()
+    torch.cuda.synchronize(dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for _ in range(reps):
+        build()
+    ev[1].record()
+    torch.cuda.synchronize(dev)
+    ms = ev[0].elapsed_time(ev[1]) / reps
+    alg = 16 * n + 8 * lsmbloom.num_words(nb)
+    res = {"workload": "C5 (configs[4]) on one GPU: %d 16-B keys into new(1e9, 0.01) = %d bits, k = %d, %d sweeps "
+                       "(lsmb_build_fixed_dev_sweep_new, as each rank at N > 1)" % (n, nb, k, nsw),
+           "value": round(n / (ms * 1e-3) / 1e6, 1), "unit": "Mkeys/s", "ms": round(ms, 3), "kernel_ms": round(ms, 3),
+           "sweeps": nsw, "strategy": lsmbloom.build_strategy(nb, n, k),
+           "roofline": leg_roofline(None, alg, ms, "build (%d sweeps of k_bin + k_apply<21> + k_ovf_apply)" % nsw)}
+    res["words_equal_oracle_fixture"] = fixture_check(w, "c5", nb)
     del w, keys
     return res
 

@@ -47,7 +47,7 @@ extern "C" {
 #define LSMB_ECORRUPT (-4) /* serialized filter fails validation               */
 #define LSMB_ENOMEM (-5)   /* device or pinned-host allocation failed          */
 
-#define LSMB_ABI_VERSION 5 /* 5: sweep builds, block CRC-32 */
+#define LSMB_ABI_VERSION 6 /* 5: sweep builds, block CRC-32; 6: fail-safe merge status words */
 
 typedef struct lsmb_ctx lsmb_ctx; /* one GPU: stream, events, scratch arenas */
 
@@ -327,8 +327,8 @@ int lsmb_multi_last_ms(lsmb_multi* m, float* out3);
  * share one), and merges with peer loads: rank g ORs word-slice g of every
  * partial into its own words (lsmb_or_gather_dev with all G sources), then
  * copies every other merged slice from its owner (one source each).  The
- * caller orders the ranks between the phases (a host barrier after each
- * rank's stream has finished).  Replaces what RCCL cannot do in one call (it
+ * caller orders the ranks between the phases: a host barrier after each
+ * rank's stream has finished, or the device flags below.  Replaces what RCCL cannot do in one call (it
  * has no bitwise-OR reduction) for the sharded flush / compaction of
  * src/db/mod.rs:377-383 and src/compaction/scheduler.rs:150-158. */
 #define LSMB_IPC_HANDLE_BYTES 64
@@ -345,20 +345,42 @@ int lsmb_ipc_import(lsmb_ctx* ctx, const uint8_t* handle, void** d_base);
 /* Unmaps an allocation lsmb_ipc_import mapped (d_base as returned). */
 int lsmb_ipc_close(lsmb_ctx* ctx, void* d_base);
 
+/* Merge status words (round 6): LSMB_MERGE_STATUS_WORDS u32 in device memory,
+ * zero when the merge is set up, owned by one merge (one per IpcMerge):
+ *   [0] poison: set (sticky) once one of the merge's phase waits timed out or
+ *       saw another rank's poison;
+ *   [1] the merge's phase waits that timed out.
+ * A poisoned merge never reads its peers' words again and leaves every range
+ * it merges all-ones: all-ones is a superset of every partial, so the filter
+ * can answer "maybe" too often but never "no" for a key that was added (a
+ * false negative would make DB::get skip the SST holding the key,
+ * src/sstable/reader.rs:196-199, src/db/mod.rs:243-267).  The caller learns
+ * of it at its next sync point (lsmb_merge_status) and must not trust the
+ * filter as exact.  The status words live in the flag allocation the peers
+ * map, so that a rank's poison is visible to every peer's waits. */
+#define LSMB_MERGE_STATUS_WORDS 2
+
 /* d_dst[i] = OR over j < nsrc of d_srcs[j][i], i < nwords (u64 words; any
  * source may be d_dst itself, or mapped peer memory).  Asynchronous on
- * `stream`.  nsrc == 1 is a copy; 1 <= nsrc <= 16. */
+ * `stream`.  nsrc == 1 is a copy; 1 <= nsrc <= 16.  d_status (NULL: none):
+ * when the merge is poisoned at kernel time, d_dst[0, nwords) = all-ones and
+ * no source is read. */
 int lsmb_or_gather_dev(lsmb_ctx* ctx, void* d_dst, const void* const* d_srcs, uint32_t nsrc, uint64_t nwords,
-                       void* stream);
+                       const uint32_t* d_status, void* stream);
 
 /* The merge's all-gather in one call: for every slice r < nsrc with
  * d_srcs[r] != NULL, d_dst[w] = d_srcs[r][w] for w in [r slice_words,
  * min((r+1) slice_words, nwords)) (u64 words; a NULL source leaves its slice
  * alone, e.g. the caller's own).  One kernel streams every slice at once, so
  * every peer link is busy.  The sources (mapped peer memory, or other local
- * buffers) must not overlap d_dst.  Asynchronous on `stream`. */
+ * buffers) must not overlap d_dst.  Asynchronous on `stream`.  d_status as
+ * above: poisoned, those slices are written all-ones. */
 int lsmb_copy_slices_dev(lsmb_ctx* ctx, void* d_dst, const void* const* d_srcs, uint32_t nsrc, uint64_t slice_words,
-                         uint64_t nwords, void* stream);
+                         uint64_t nwords, const uint32_t* d_status, void* stream);
+
+/* The merge's last step: if the merge is poisoned once everything before this
+ * on `stream` has run, d_words[0, nwords) = all-ones; otherwise nothing. */
+int lsmb_poison_fill_dev(lsmb_ctx* ctx, void* d_words, uint64_t nwords, const uint32_t* d_status, void* stream);
 
 /* Device-ordered phases for the merge above, so that no host waits inside it:
  * a flag is a u32 epoch counter in device memory (this process's own, or a
@@ -366,22 +388,28 @@ int lsmb_copy_slices_dev(lsmb_ctx* ctx, void* d_dst, const void* const* d_srcs, 
  *   signal(own flag[0], e); wait(every rank's flag[0] >= e)   partials final
  *   or_gather (reduce-scatter);  signal(flag[1], e); wait(all flag[1] >= e)
  *   copy_slices (all-gather); signal(flag[2], e); wait(all flag[2] >= e)
- * (lsmbloom.dist.IpcMerge).  All enqueue and return at once. */
+ *   poison_fill
+ * (lsmbloom.dist.IpcMerge, lsmbloom.dist.merge_schedule).  All enqueue and
+ * return at once. */
 
 /* After everything before it on `stream`: a system-scope release store of
  * `value` into *d_flag. */
 int lsmb_flag_signal_dev(lsmb_ctx* ctx, uint32_t* d_flag, uint32_t value, void* stream);
 
 /* Later work on `stream` waits until every d_flags[j] >= value (epoch compare,
- * wrap-safe), j < nflags <= 64.  A flag still short after timeout_ms counts
- * one timeout (lsmb_flag_timeouts) and the wait ends anyway: a dead peer can
- * never hang the queue. */
-int lsmb_flag_wait_dev(lsmb_ctx* ctx, const uint32_t* const* d_flags, uint32_t nflags, uint32_t value,
-                       uint32_t timeout_ms, void* stream);
+ * wrap-safe), j < nflags <= 64.  d_poison[j] (or NULL) = rank j's poison word
+ * (its status word [0]; the caller's own among them).  The wait ends early,
+ * and poisons this merge (d_status[0] = 1), when any poison word is set, also
+ * when one is set after the flags were met; a flag still short after
+ * timeout_ms counts a timeout (d_status[1] += 1), poisons the merge and ends
+ * the wait: a dead peer can never hang the queue, and never yields a filter
+ * with missing bits. */
+int lsmb_flag_wait_dev(lsmb_ctx* ctx, const uint32_t* const* d_flags, const uint32_t* const* d_poison, uint32_t nflags,
+                       uint32_t value, uint32_t timeout_ms, uint32_t* d_status, void* stream);
 
-/* Waits of this context that timed out so far (a synchronous read: call it
- * after the streams that waited have finished). */
-int lsmb_flag_timeouts(lsmb_ctx* ctx, uint32_t* count);
+/* The merge's sync point: waits for `stream`, then out2 = {poison, timeouts}
+ * (the status words above). */
+int lsmb_merge_status(lsmb_ctx* ctx, const uint32_t* d_status, void* stream, uint32_t* out2);
 
 /* ---- device-resident filter sets (multi-get pre-check) --------------------- */
 /* An lsmb_fset keeps up to 64 SSTable filters resident in device memory, each

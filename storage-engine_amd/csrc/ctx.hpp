@@ -100,7 +100,6 @@ struct lsmb_ctx {
     lsmb::DevBuf crc_parts;              // CRC-32 workgroup partials (crc32.hip)
     lsmb::DevBuf ws_hashes;              // k_hash records (var-len / odd-length keys)
     lsmb::DevBuf err;                    // LSMB_STATS builds: pass A's overflow counters
-    lsmb::DevBuf flag_timeouts;          // lsmb_flag_wait_dev: waits that timed out (u32, zeroed at allocation)
     lsmb::DevBuf ws_ovf, ws_dirty;       // partition: overflow words + unit marks (all-zero between builds)
     lsmb::DevBuf ws_ovl, ws_ovn;         // fresh partition builds: overflow position lists + lengths
     // The workspace above is shared by every build on this context, whatever

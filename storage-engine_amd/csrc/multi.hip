@@ -41,15 +41,40 @@ struct OrSources {
     uint32_t n;
 };
 
+// The merge's fail-safe (round 6).  `status` (may be null) is the merge's
+// status words: status[0] != 0 = poisoned (a phase wait timed out or saw a
+// peer's poison; k_flag_wait).  A poisoned merge must not read its peers'
+// words (they may be mid-rewrite) and must never leave a bit unset that the
+// true merge would set: it writes all-ones instead, the one value that is a
+// superset of every partial, so the filter then answers "maybe" for every key
+// (false positives only, never a false negative: src/sstable/reader.rs:196-199).
+__device__ __forceinline__ bool poisoned(const uint32_t* status) {
+    return status && __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+}
+
+template <class V>
+__device__ __forceinline__ V all_ones() {
+    if constexpr (sizeof(V) == 16) {
+        return V{~0u, ~0u, ~0u, ~0u};
+    } else {
+        return ~V(0);
+    }
+}
+
 // dst[i] = OR over j of src_j[i], i < count (elements of V).  dst may be one
 // of the sources (the owner's own partial): each element is read by every
 // source load before its one store, by the same thread.  So dst is not
 // __restrict__ (it aliases a source).  N > 0: N sources known at compile
 // time, so a thread's N loads (over N peer links) are all in flight before
-// the first OR; N = 0: a runtime count (9..16 sources).
+// the first OR; N = 0: a runtime count (9..16 sources).  Poisoned: all-ones.
 template <class V, int N>
-__global__ __launch_bounds__(256) void k_or_gather(V* dst, OrSources src, uint64_t count) {
+__global__ __launch_bounds__(256) void k_or_gather(V* dst, OrSources src, uint64_t count, const uint32_t* status) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (poisoned(status)) {
+        for (; i < count; i += stride) dst[i] = all_ones<V>();
+        return;
+    }
     auto orv = [](V& v, const V& x) {
         if constexpr (sizeof(V) == 16) {
             v.x |= x.x, v.y |= x.y, v.z |= x.z, v.w |= x.w;
@@ -57,7 +82,7 @@ __global__ __launch_bounds__(256) void k_or_gather(V* dst, OrSources src, uint64
             v |= x;
         }
     };
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
+    for (; i < count; i += stride) {
         V v = static_cast<const V*>(src.p[0])[i];
         if constexpr (N > 0) {
             V w[N];
@@ -77,14 +102,19 @@ __global__ __launch_bounds__(256) void k_or_gather(V* dst, OrSources src, uint64
 // (src.p[r] == nullptr: the caller's own slice, left alone).  blockIdx.y is
 // the slice, so every peer link streams at once (one copy per peer, one
 // after another on a stream, would use one link at a time).  Four elements
-// in flight per thread.
+// in flight per thread.  Poisoned: the slices are written all-ones.
 template <class V>
-__global__ __launch_bounds__(256) void k_copy_slices(V* __restrict__ dst, OrSources src, uint64_t per, uint64_t count) {
+__global__ __launch_bounds__(256) void k_copy_slices(V* __restrict__ dst, OrSources src, uint64_t per, uint64_t count,
+                                                     const uint32_t* status) {
     const V* __restrict__ s = static_cast<const V*>(src.p[blockIdx.y]);
     if (!s) return;  // (block-uniform)
     const uint64_t a = (uint64_t)blockIdx.y * per, b = min(count, a + per);
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint64_t i = a + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (poisoned(status)) {
+        for (; i < b; i += stride) dst[i] = all_ones<V>();
+        return;
+    }
     for (; i + 3 * stride < b; i += 4 * stride) {
         V x[4];
 #pragma unroll
@@ -95,16 +125,34 @@ __global__ __launch_bounds__(256) void k_copy_slices(V* __restrict__ dst, OrSour
     for (; i < b; i += stride) dst[i] = s[i];
 }
 
+// The merge's last step: a merge that ended poisoned (at any of its waits,
+// the last included) leaves its whole range all-ones.  Not poisoned: every
+// block reads the status word and ends.
+__global__ __launch_bounds__(256) void k_poison_fill(uint64_t* words, uint64_t count, const uint32_t* status) {
+    if (!poisoned(status)) return;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) words[i] = ~0ull;
+}
+
 // ---- device-ordered phase flags (cross-process merge, lsmb_flag_*) --------
 // A flag is a u32 epoch counter in device memory (this process's, or a peer's
 // mapped over IPC).  signal: one system-scope release store of the epoch after
 // everything before it on the stream (kernel boundaries already release each
 // kernel's stores at agent scope, i.e. L2 written back across the XCDs).
 // wait: one wave, lane j polls flag j with system-scope loads (no stale L2
-// copy) until it reaches the epoch (wrap-safe compare), backing off with
-// s_sleep; every lane gives up after `ticks` of the constant-rate wall clock
-// and counts a timeout instead, so the kernel always ends (a peer that died
-// cannot hang the queue).
+// copy) until every flag reaches the epoch (wrap-safe compare), backing off
+// with s_sleep.  The wait is the merge's fail-safe (round 6):
+//   * it gives up after `ticks` of the constant-rate wall clock (a peer that
+//     died cannot hang the queue), counts the timeout in status[1] and
+//     poisons the merge (status[0] = 1, a system-scope store: the status
+//     words sit in the flag array the peers map, so they see it);
+//   * it also ends as soon as any rank's poison word (poison[j], this rank's
+//     own among them) is set, and reads every poison word once more after the
+//     flags were met: a peer that gave up on us may already be rewriting the
+//     words we read, and its poison is published before that rewrite, so the
+//     next wait after such a read sees it and poisons this merge too.
+// A poisoned merge writes all-ones instead of reading peers (k_or_gather,
+// k_copy_slices) and ends with its range all-ones (k_poison_fill).
 constexpr uint32_t kMaxFlags = 64;
 struct FlagSet {
     const uint32_t* p[kMaxFlags];
@@ -115,41 +163,58 @@ __global__ __launch_bounds__(64) void k_flag_signal(uint32_t* flag, uint32_t val
     if (threadIdx.x == 0) __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(64) void k_flag_wait(FlagSet fs, uint32_t value, uint64_t ticks, uint32_t* timeouts) {
+__device__ __forceinline__ uint32_t load_sys(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(64) void k_flag_wait(FlagSet fs, FlagSet ps, uint32_t value, uint64_t ticks,
+                                                  uint32_t* status) {
     const uint32_t j = threadIdx.x;
-    if (j < fs.n) {
-        const uint64_t t0 = (uint64_t)wall_clock64();
-        for (;;) {
-            const uint32_t v = __hip_atomic_load(fs.p[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            if ((int32_t)(v - value) >= 0) break;
-            if ((uint64_t)wall_clock64() - t0 > ticks) {
-                atomicAdd(timeouts, 1u);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(8);
+    // the loop is wave-uniform: its exits are ballots and the scalar wall clock
+    bool met = j >= fs.n;
+    bool timed_out = false, poison = false;
+    const uint64_t t0 = (uint64_t)wall_clock64();
+    for (;;) {
+        if (!met) met = (int32_t)(load_sys(fs.p[j]) - value) >= 0;
+        const bool pz = j < ps.n && load_sys(ps.p[j]) != 0;
+        if (__ballot(pz)) {
+            poison = true;
+            break;
         }
+        if (__ballot(!met) == 0) break;
+        if ((uint64_t)wall_clock64() - t0 > ticks) {
+            timed_out = true;
+            break;
+        }
+        __builtin_amdgcn_s_sleep(8);
+    }
+    if (!poison && __ballot(j < ps.n && load_sys(ps.p[j]) != 0)) poison = true;
+    if (j == 0 && (timed_out || poison)) {
+        if (timed_out) atomicAdd(&status[1], 1u);
+        __hip_atomic_store(&status[0], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: later reads see the peers' data
 }
 
 template <class V>
-hipError_t or_gather_n(V* dst, const OrSources& s, uint64_t count, uint32_t g, hipStream_t st) {
+hipError_t or_gather_n(V* dst, const OrSources& s, uint64_t count, uint32_t g, const uint32_t* status, hipStream_t st) {
     const dim3 grid(g), block(256);
     switch (s.n) {
-        case 1: k_or_gather<V, 1><<<grid, block, 0, st>>>(dst, s, count); break;
-        case 2: k_or_gather<V, 2><<<grid, block, 0, st>>>(dst, s, count); break;
-        case 3: k_or_gather<V, 3><<<grid, block, 0, st>>>(dst, s, count); break;
-        case 4: k_or_gather<V, 4><<<grid, block, 0, st>>>(dst, s, count); break;
-        case 5: k_or_gather<V, 5><<<grid, block, 0, st>>>(dst, s, count); break;
-        case 6: k_or_gather<V, 6><<<grid, block, 0, st>>>(dst, s, count); break;
-        case 7: k_or_gather<V, 7><<<grid, block, 0, st>>>(dst, s, count); break;
-        case 8: k_or_gather<V, 8><<<grid, block, 0, st>>>(dst, s, count); break;
-        default: k_or_gather<V, 0><<<grid, block, 0, st>>>(dst, s, count); break;
+        case 1: k_or_gather<V, 1><<<grid, block, 0, st>>>(dst, s, count, status); break;
+        case 2: k_or_gather<V, 2><<<grid, block, 0, st>>>(dst, s, count, status); break;
+        case 3: k_or_gather<V, 3><<<grid, block, 0, st>>>(dst, s, count, status); break;
+        case 4: k_or_gather<V, 4><<<grid, block, 0, st>>>(dst, s, count, status); break;
+        case 5: k_or_gather<V, 5><<<grid, block, 0, st>>>(dst, s, count, status); break;
+        case 6: k_or_gather<V, 6><<<grid, block, 0, st>>>(dst, s, count, status); break;
+        case 7: k_or_gather<V, 7><<<grid, block, 0, st>>>(dst, s, count, status); break;
+        case 8: k_or_gather<V, 8><<<grid, block, 0, st>>>(dst, s, count, status); break;
+        default: k_or_gather<V, 0><<<grid, block, 0, st>>>(dst, s, count, status); break;
     }
     return hipGetLastError();
 }
 
-hipError_t launch_or_gather(uint64_t* dst, const OrSources& s, uint64_t nwords, int num_cus, hipStream_t st) {
+hipError_t launch_or_gather(uint64_t* dst, const OrSources& s, uint64_t nwords, int num_cus, hipStream_t st,
+                            const uint32_t* status = nullptr) {
     if (nwords == 0) return hipSuccess;
     bool a16 = ((uintptr_t)dst & 15) == 0 && (nwords & 1) == 0;
     for (uint32_t j = 0; j < s.n; j++) a16 = a16 && ((uintptr_t)s.p[j] & 15) == 0;
@@ -157,13 +222,13 @@ hipError_t launch_or_gather(uint64_t* dst, const OrSources& s, uint64_t nwords, 
     uint64_t g = (count + 255) / 256;
     g = std::min<uint64_t>(g, (uint64_t)num_cus * 8);
     if (g < 1) g = 1;
-    if (a16) return or_gather_n((uint4*)dst, s, count, (uint32_t)g, st);
-    return or_gather_n(dst, s, count, (uint32_t)g, st);
+    if (a16) return or_gather_n((uint4*)dst, s, count, (uint32_t)g, status, st);
+    return or_gather_n(dst, s, count, (uint32_t)g, status, st);
 }
 
 // dst words of slice r (slice_words each, nwords in all) from s.p[r] where set.
 hipError_t launch_copy_slices(uint64_t* dst, const OrSources& s, uint64_t slice_words, uint64_t nwords, int num_cus,
-                              hipStream_t st) {
+                              hipStream_t st, const uint32_t* status = nullptr) {
     if (nwords == 0 || s.n == 0) return hipSuccess;
     bool a16 = ((uintptr_t)dst & 15) == 0 && (nwords & 1) == 0 && (slice_words & 1) == 0;
     for (uint32_t j = 0; j < s.n; j++) a16 = a16 && ((uintptr_t)s.p[j] & 15) == 0;
@@ -173,9 +238,9 @@ hipError_t launch_copy_slices(uint64_t* dst, const OrSources& s, uint64_t slice_
     if (gx < 1) gx = 1;
     const dim3 grid((uint32_t)gx, s.n);
     if (a16)
-        k_copy_slices<uint4><<<grid, dim3(256), 0, st>>>((uint4*)dst, s, per, count);
+        k_copy_slices<uint4><<<grid, dim3(256), 0, st>>>((uint4*)dst, s, per, count, status);
     else
-        k_copy_slices<uint64_t><<<grid, dim3(256), 0, st>>>(dst, s, per, count);
+        k_copy_slices<uint64_t><<<grid, dim3(256), 0, st>>>(dst, s, per, count, status);
     return hipGetLastError();
 }
 
@@ -521,7 +586,7 @@ int lsmb_ipc_close(lsmb_ctx* c, void* d_base) {
 }
 
 int lsmb_or_gather_dev(lsmb_ctx* c, void* d_dst, const void* const* d_srcs, uint32_t nsrc, uint64_t nwords,
-                       void* stream) {
+                       const uint32_t* d_status, void* stream) {
     if (!c || !d_srcs) return fail(LSMB_EINVAL, "null argument");
     if (nsrc < 1 || nsrc > (uint32_t)kMaxShards) return fail(LSMB_EINVAL, "nsrc must be in [1, %d]", kMaxShards);
     if (nwords == 0) return LSMB_OK;
@@ -534,13 +599,14 @@ int lsmb_or_gather_dev(lsmb_ctx* c, void* d_dst, const void* const* d_srcs, uint
         s.p[j] = d_srcs[j];
     }
     if (((uintptr_t)d_dst & 7) != 0) return fail(LSMB_EINVAL, "d_dst is not 8-byte aligned");
+    if (((uintptr_t)d_status & 3) != 0) return fail(LSMB_EINVAL, "d_status is not 4-byte aligned");
     DevGuard g(c->dev);
-    HIP_TRY(launch_or_gather((uint64_t*)d_dst, s, nwords, c->num_cus, pick_stream(c, stream)));
+    HIP_TRY(launch_or_gather((uint64_t*)d_dst, s, nwords, c->num_cus, pick_stream(c, stream), d_status));
     return LSMB_OK;
 }
 
 int lsmb_copy_slices_dev(lsmb_ctx* c, void* d_dst, const void* const* d_srcs, uint32_t nsrc, uint64_t slice_words,
-                         uint64_t nwords, void* stream) {
+                         uint64_t nwords, const uint32_t* d_status, void* stream) {
     if (!c || !d_srcs) return fail(LSMB_EINVAL, "null argument");
     if (nsrc < 1 || nsrc > (uint32_t)kMaxShards) return fail(LSMB_EINVAL, "nsrc must be in [1, %d]", kMaxShards);
     if (nwords == 0) return LSMB_OK;
@@ -553,8 +619,22 @@ int lsmb_copy_slices_dev(lsmb_ctx* c, void* d_dst, const void* const* d_srcs, ui
         s.p[j] = d_srcs[j];
     }
     if (((uintptr_t)d_dst & 7) != 0) return fail(LSMB_EINVAL, "d_dst is not 8-byte aligned");
+    if (((uintptr_t)d_status & 3) != 0) return fail(LSMB_EINVAL, "d_status is not 4-byte aligned");
     DevGuard g(c->dev);
-    HIP_TRY(launch_copy_slices((uint64_t*)d_dst, s, slice_words, nwords, c->num_cus, pick_stream(c, stream)));
+    HIP_TRY(launch_copy_slices((uint64_t*)d_dst, s, slice_words, nwords, c->num_cus, pick_stream(c, stream), d_status));
+    return LSMB_OK;
+}
+
+int lsmb_poison_fill_dev(lsmb_ctx* c, void* d_words, uint64_t nwords, const uint32_t* d_status, void* stream) {
+    if (!c || !d_status) return fail(LSMB_EINVAL, "null argument");
+    if (nwords == 0) return LSMB_OK;
+    if (!d_words || ((uintptr_t)d_words & 7) != 0) return fail(LSMB_EINVAL, "d_words: null or not 8-byte aligned");
+    if (((uintptr_t)d_status & 3) != 0) return fail(LSMB_EINVAL, "d_status is not 4-byte aligned");
+    DevGuard g(c->dev);
+    // a small grid: when the merge is healthy every block only reads the status
+    const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((nwords + 255) / 256, (uint64_t)c->num_cus));
+    k_poison_fill<<<dim3((uint32_t)blocks), dim3(256), 0, pick_stream(c, stream)>>>((uint64_t*)d_words, nwords, d_status);
+    HIP_TRY(hipGetLastError());
     return LSMB_OK;
 }
 
@@ -567,40 +647,39 @@ int lsmb_flag_signal_dev(lsmb_ctx* c, uint32_t* d_flag, uint32_t value, void* st
     return LSMB_OK;
 }
 
-int lsmb_flag_wait_dev(lsmb_ctx* c, const uint32_t* const* d_flags, uint32_t nflags, uint32_t value,
-                       uint32_t timeout_ms, void* stream) {
-    if (!c || !d_flags) return fail(LSMB_EINVAL, "null argument");
+int lsmb_flag_wait_dev(lsmb_ctx* c, const uint32_t* const* d_flags, const uint32_t* const* d_poison, uint32_t nflags,
+                       uint32_t value, uint32_t timeout_ms, uint32_t* d_status, void* stream) {
+    if (!c || !d_flags || !d_status) return fail(LSMB_EINVAL, "null argument");
     if (nflags > kMaxFlags) return fail(LSMB_EINVAL, "nflags must be at most %u", kMaxFlags);
-    if (nflags == 0) return LSMB_OK;
-    FlagSet fs;
+    if (((uintptr_t)d_status & 3) != 0) return fail(LSMB_EINVAL, "d_status is not 4-byte aligned");
+    FlagSet fs, ps;
     fs.n = nflags;
+    ps.n = d_poison ? nflags : 0;
     for (uint32_t j = 0; j < nflags; j++) {
         if (!d_flags[j] || ((uintptr_t)d_flags[j] & 3) != 0) return fail(LSMB_EINVAL, "flag %u: null or unaligned", j);
         fs.p[j] = d_flags[j];
+        if (d_poison) {
+            if (!d_poison[j] || ((uintptr_t)d_poison[j] & 3) != 0)
+                return fail(LSMB_EINVAL, "poison word %u: null or unaligned", j);
+            ps.p[j] = d_poison[j];
+        }
     }
     DevGuard g(c->dev);
-    hipStream_t st = pick_stream(c, stream);
-    if (!c->flag_timeouts.p) {
-        HIP_TRY(c->flag_timeouts.ensure(64));
-        HIP_TRY(hipMemsetAsync(c->flag_timeouts.p, 0, 64, st));  // once per context, before the first wait
-    }
     int khz = 0;
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->dev) != hipSuccess || khz <= 0) khz = 100000;
     const uint64_t ticks = (uint64_t)timeout_ms * (uint64_t)khz;
-    k_flag_wait<<<dim3(1), dim3(64), 0, st>>>(fs, value, ticks, (uint32_t*)c->flag_timeouts.p);
+    k_flag_wait<<<dim3(1), dim3(64), 0, pick_stream(c, stream)>>>(fs, ps, value, ticks, d_status);
     HIP_TRY(hipGetLastError());
     return LSMB_OK;
 }
 
-int lsmb_flag_timeouts(lsmb_ctx* c, uint32_t* count) {
-    if (!c || !count) return fail(LSMB_EINVAL, "null argument");
-    *count = 0;
-    if (!c->flag_timeouts.p) return LSMB_OK;
+int lsmb_merge_status(lsmb_ctx* c, const uint32_t* d_status, void* stream, uint32_t* out2) {
+    if (!c || !d_status || !out2) return fail(LSMB_EINVAL, "null argument");
+    if (((uintptr_t)d_status & 3) != 0) return fail(LSMB_EINVAL, "d_status is not 4-byte aligned");
     DevGuard g(c->dev);
-    // (the caller has finished the streams that waited; c->st orders this read
-    // after the zeroing when both ran on it)
-    HIP_TRY(hipMemcpyAsync(count, c->flag_timeouts.p, 4, hipMemcpyDeviceToHost, c->st));
-    HIP_TRY(hipStreamSynchronize(c->st));
+    const hipStream_t st = pick_stream(c, stream);
+    HIP_TRY(hipMemcpyAsync(out2, d_status, 8, hipMemcpyDeviceToHost, st));  // after the stream's waits
+    HIP_TRY(hipStreamSynchronize(st));
     return LSMB_OK;
 }
 

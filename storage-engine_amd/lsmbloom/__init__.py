@@ -111,13 +111,14 @@ SIGNATURES = {
     "lsmb_ipc_export": (ctypes.c_int, [vp, u8p, u64p]),
     "lsmb_ipc_import": (ctypes.c_int, [vp, u8p, ctypes.POINTER(vp)]),
     "lsmb_ipc_close": (ctypes.c_int, [vp, vp]),
-    "lsmb_or_gather_dev": (ctypes.c_int, [vp, vp, ctypes.POINTER(vp), ctypes.c_uint32, ctypes.c_uint64, vp]),
+    "lsmb_or_gather_dev": (ctypes.c_int, [vp, vp, ctypes.POINTER(vp), ctypes.c_uint32, ctypes.c_uint64, vp, vp]),
     "lsmb_copy_slices_dev": (ctypes.c_int, [vp, vp, ctypes.POINTER(vp), ctypes.c_uint32, ctypes.c_uint64,
-                                            ctypes.c_uint64, vp]),
+                                            ctypes.c_uint64, vp, vp]),
+    "lsmb_poison_fill_dev": (ctypes.c_int, [vp, vp, ctypes.c_uint64, vp, vp]),
     "lsmb_flag_signal_dev": (ctypes.c_int, [vp, vp, ctypes.c_uint32, vp]),
-    "lsmb_flag_wait_dev": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
-                                          vp]),
-    "lsmb_flag_timeouts": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint32)]),
+    "lsmb_flag_wait_dev": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.c_uint32, ctypes.c_uint32,
+                                          ctypes.c_uint32, vp, vp]),
+    "lsmb_merge_status": (ctypes.c_int, [vp, vp, vp, u32p]),
     "lsmb_stream_open": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(vp)]),
     "lsmb_stream_reset": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32]),
     "lsmb_stream_close": (None, [vp]),
@@ -384,36 +385,48 @@ class Context:
         _check(lib().lsmb_or_reduce_dev(self.h, vp(dst.data_ptr()), vp(src.data_ptr()), nwords, nsrc,
                                         stride_words, self._stream(stream)))
 
-    def or_gather_dev(self, dst_ptr, src_ptrs, nwords, stream=None):
+    def or_gather_dev(self, dst_ptr, src_ptrs, nwords, stream=None, status_ptr=0):
         """dst[i] = OR of src_j[i] over the raw device pointers src_ptrs (own or
-        IPC-mapped peer memory), nwords u64 words (lsmb_or_gather_dev)."""
+        IPC-mapped peer memory), nwords u64 words (lsmb_or_gather_dev); with a
+        merge's status words (status_ptr) a poisoned merge writes all-ones."""
         arr = (vp * len(src_ptrs))(*[vp(int(p)) for p in src_ptrs])
         _check(lib().lsmb_or_gather_dev(self.h, vp(int(dst_ptr)), arr, len(src_ptrs), int(nwords),
-                                        self._stream(stream)))
+                                        vp(int(status_ptr or 0)), self._stream(stream)))
 
-    def copy_slices_dev(self, dst_ptr, src_ptrs, slice_words, nwords, stream=None):
+    def copy_slices_dev(self, dst_ptr, src_ptrs, slice_words, nwords, stream=None, status_ptr=0):
         """dst slice r = src_ptrs[r]'s slice r (u64 words) for every r whose source is
         not None/0: the merge's all-gather in one kernel (lsmb_copy_slices_dev)."""
         arr = (vp * len(src_ptrs))(*[vp(int(p or 0)) for p in src_ptrs])
         _check(lib().lsmb_copy_slices_dev(self.h, vp(int(dst_ptr)), arr, len(src_ptrs), int(slice_words), int(nwords),
+                                          vp(int(status_ptr or 0)), vp(stream or 0)))
+
+    def poison_fill_dev(self, words_ptr, nwords, status_ptr, stream=None):
+        """The merge's last step: all-ones over nwords words if the merge is
+        poisoned (lsmb_poison_fill_dev)."""
+        _check(lib().lsmb_poison_fill_dev(self.h, vp(int(words_ptr)), int(nwords), vp(int(status_ptr)),
                                           vp(stream or 0)))
 
     def flag_signal_dev(self, flag_ptr, value, stream=None):
         """After the stream's prior work: *flag = value, system-scope release (lsmb_flag_signal_dev)."""
         _check(lib().lsmb_flag_signal_dev(self.h, vp(int(flag_ptr)), int(value) & 0xFFFFFFFF, vp(stream or 0)))
 
-    def flag_wait_dev(self, flag_ptrs, value, timeout_ms=20000, stream=None):
-        """Later work on the stream waits until every flag >= value, or timeout_ms
-        (then counted in flag_timeouts()) (lsmb_flag_wait_dev)."""
+    def flag_wait_dev(self, flag_ptrs, value, status_ptr, timeout_ms=20000, poison_ptrs=None, stream=None):
+        """Later work on the stream waits until every flag >= value; a timeout or
+        a set poison word ends the wait and poisons the merge's status words
+        (lsmb_flag_wait_dev)."""
         arr = (vp * len(flag_ptrs))(*[vp(int(p)) for p in flag_ptrs])
-        _check(lib().lsmb_flag_wait_dev(self.h, arr, len(flag_ptrs), int(value) & 0xFFFFFFFF, int(timeout_ms),
-                                        vp(stream or 0)))
+        parr = (vp * len(flag_ptrs))(*[vp(int(p)) for p in poison_ptrs]) if poison_ptrs else None
+        if poison_ptrs and len(poison_ptrs) != len(flag_ptrs):
+            raise ValueError("one poison word per flag")
+        _check(lib().lsmb_flag_wait_dev(self.h, arr, parr, len(flag_ptrs), int(value) & 0xFFFFFFFF, int(timeout_ms),
+                                        vp(int(status_ptr)), vp(stream or 0)))
 
-    def flag_timeouts(self):
-        """Flag waits of this context that timed out so far (lsmb_flag_timeouts)."""
-        n = ctypes.c_uint32(0)
-        _check(lib().lsmb_flag_timeouts(self.h, ctypes.byref(n)))
-        return int(n.value)
+    def merge_status(self, status_ptr, stream=None):
+        """(poisoned, timed-out waits) of a merge's status words, after the
+        stream's pending work (lsmb_merge_status: synchronises the stream)."""
+        out = (ctypes.c_uint32 * 2)()
+        _check(lib().lsmb_merge_status(self.h, vp(int(status_ptr)), vp(stream or 0), out))
+        return int(out[0]), int(out[1])
 
     def ipc_import(self, handle):
         """Maps another process's device allocation (lsmb_ipc_import) -> base pointer (int)."""

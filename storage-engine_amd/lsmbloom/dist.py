@@ -82,6 +82,22 @@ def or_allreduce_(words, group=None, ctx=None):
     return words
 
 
+class MergePoisoned(RuntimeError):
+    """An IpcMerge whose phase waits timed out (a peer died or stalled past
+    timeout_ms) or that saw another rank's poison.  Its ranges were written
+    all-ones from that point on, so the filter has no false negatives, but it
+    is not the exact merge: do not serialize it as the run's filter."""
+
+
+# A rank's flag array (device int32, exported to the peers): the three phase
+# epochs, then the merge's status words (include/lsmbloom.h,
+# LSMB_MERGE_STATUS_WORDS): poison (published to the peers) and timed-out waits.
+_PHASES = 3
+_POISON = 3
+_TIMEOUTS = 4
+_FLAG_WORDS = 8
+
+
 class IpcMerge:
     """The OR-allreduce by peer loads between processes (one per GPU), with no
     collective library on the data path (include/lsmbloom.h, "cross-process
@@ -95,25 +111,35 @@ class IpcMerge:
     Per GPU it reads (G-1)/G of the range twice over the peer links, the RCCL
     path's bytes.
 
-    Ordering (ordered="device", the default): the phases are ordered on the
-    GPUs, never on the host.  Every rank also exports a 3-word flag array; merge
-    number e enqueues on the caller's stream
+    Ordering.  ordered="host" (the default): a stream synchronise plus a
+    `group` barrier between phases.  ordered="device": the phases are ordered
+    on the GPUs, never on the host.  Every rank also exports a flag array;
+    merge number e enqueues on the caller's stream
         signal(my flag[0] = e); wait(every rank's flag[0] >= e)   partials final
         reduce-scatter;  signal(flag[1] = e); wait(all flag[1] >= e)
         all-gather;      signal(flag[2] = e); wait(all flag[2] >= e)
+        poison fill
     (lsmb_flag_signal_dev / lsmb_flag_wait_dev) and returns at once: the host
     never synchronises inside a merge, so a sweep's merge overlaps the next
     sweep's build.  The last wait keeps any later work on the stream from
-    rewriting my words while a peer may still read them.  A wait that times
-    out (a dead peer) is counted, not hung on: close() / timeouts() report it.
-    `merge_schedule` below is the protocol as data (tests/test_ipc_protocol.py
-    runs it against simulated ranks).  ordered="host" is the round-4 form: a
-    stream synchronise plus a `group` barrier between phases.
+    rewriting my words while a peer may still read them.  `merge_schedule`
+    below is the protocol as data (tests/test_ipc_protocol.py runs it against
+    simulated ranks).  The device-ordered form has run with every rank on one
+    GPU only; bench.py selects it explicitly, after checking its words against
+    RCCL's on the node it runs on.
+
+    Fail-safe (device-ordered).  A wait that times out (a dead or stalled
+    peer), or that sees another rank's poison word, poisons this merge for
+    good: from then on its kernels read no peer words and write all-ones, and
+    the merge's range ends all-ones — a superset of every partial, so the
+    filter may answer "maybe" too often but never "no" for an added key.  The
+    error surfaces at the next sync point: allreduce(..., check=True),
+    check(), or close().
 
     `group` (gloo) exchanges the handles once, checks each new word range once
     against every rank's, and orders close()."""
 
-    def __init__(self, words, ctx, group=None, ordered="device", timeout_ms=20000):
+    def __init__(self, words, ctx, group=None, ordered="host", timeout_ms=20000):
         import lsmbloom
         if ordered not in ("device", "host"):
             raise ValueError("ordered must be 'device' or 'host'")
@@ -123,9 +149,9 @@ class IpcMerge:
         self.rank = dist.get_rank(group)
         self.epoch = 0
         self._checked = set()
-        # phase flags (epochs), zero before any peer can poll them: the handle
-        # exchange below happens after this synchronise
-        self.flags = torch.zeros(4, dtype=torch.int32, device=words.device)
+        # phase flags (epochs) and status words, zero before any peer can poll
+        # them: the handle exchange below happens after this synchronise
+        self.flags = torch.zeros(_FLAG_WORDS, dtype=torch.int32, device=words.device)
         torch.cuda.synchronize(words.device)
         h, off = lsmbloom.ipc_export(words)
         fh, foff = lsmbloom.ipc_export(self.flags)
@@ -148,23 +174,39 @@ class IpcMerge:
                 fbase = ctx.ipc_import(fhh)
                 self.bases.append(fbase)
                 self.fptrs.append(fbase + foo)
+        self.status_ptr = self.fptrs[self.rank] + 4 * _POISON
 
-    def timeouts(self):
-        """Flag waits that timed out so far on this rank (the caller has
-        finished the merging streams)."""
-        return self.ctx.flag_timeouts()
+    def status(self, stream=None):
+        """(poisoned, timed-out waits) of this merge so far, after `stream`'s
+        pending work (default: the current stream; synchronises it)."""
+        stream = stream or torch.cuda.current_stream(self.words.device)
+        p, t = self.ctx.merge_status(self.status_ptr, stream=stream.cuda_stream)
+        return bool(p), t
+
+    def timeouts(self, stream=None):
+        """Phase waits of this merge that timed out so far."""
+        return self.status(stream)[1]
+
+    def check(self, stream=None):
+        """The merge's sync point: raises MergePoisoned if any merge so far was
+        poisoned (its ranges are all-ones, not the exact OR)."""
+        p, t = self.status(stream)
+        if p:
+            raise MergePoisoned("IpcMerge rank %d: merge poisoned (%d phase waits timed out here; a peer died, "
+                                "stalled past %d ms or was poisoned itself); the merged ranges are all-ones"
+                                % (self.rank, t, self.timeout_ms))
 
     def close(self, check=True):
         """Unmaps the peers (after a barrier: no peer reads my words any more);
-        raises if any phase wait timed out, unless check=False."""
+        raises MergePoisoned if the merge was poisoned, unless check=False."""
         torch.cuda.synchronize(self.words.device)
         dist.barrier(group=self.group)
-        n = self.ctx.flag_timeouts()
+        poisoned, n = self.status()
         for b in self.bases:
             self.ctx.ipc_close(b)
         self.bases, self.ptrs, self.fptrs = [], [], []
-        if n and check:
-            raise RuntimeError("IpcMerge: %d phase waits timed out (a peer never signalled)" % n)
+        if poisoned and check:
+            raise MergePoisoned("IpcMerge: merge poisoned, %d phase waits timed out on this rank" % n)
 
     def _phase_done(self, stream):
         stream.synchronize()
@@ -182,12 +224,13 @@ class IpcMerge:
             raise ValueError("ranks disagree on the word range: this rank [%d, %d)" % (lo, hi))
         self._checked.add((lo, hi))
 
-    def allreduce(self, lo=0, hi=None, stream=None):
+    def allreduce(self, lo=0, hi=None, stream=None, check=False):
         """In-place OR-allreduce of words[lo:hi] (word indices) over the group,
         after the caller's pending work on `stream` (default: current).
         ordered="device": enqueued only (returns at once); the stream's later
         work sees the merged range.  ordered="host": returns when every rank's
-        range is merged."""
+        range is merged.  check=True: also waits for the stream and raises
+        MergePoisoned if the merge (or an earlier one) was poisoned."""
         hi = self.words.numel() if hi is None else hi
         if not 0 <= lo <= hi <= self.words.numel():
             raise ValueError("word range [%d, %d) outside this rank's %d words" % (lo, hi, self.words.numel()))
@@ -200,41 +243,52 @@ class IpcMerge:
                     self._gather(op, stream)
                 elif op[0] == "wait" and op[1] in (1, 2):
                     self._phase_done(stream)
-            return self.words
-        self.epoch += 1
-        for op in merge_schedule(self.rank, self.world, lo, hi, self.epoch):
-            if op[0] == "signal":
-                _, ph, e = op
-                self.ctx.flag_signal_dev(self.fptrs[self.rank] + 4 * ph, e, stream=stream.cuda_stream)
-            elif op[0] == "wait":
-                _, ph, e = op
-                self.ctx.flag_wait_dev([p + 4 * ph for p in self.fptrs], e, self.timeout_ms,
-                                       stream=stream.cuda_stream)
-            else:
-                self._gather(op, stream)
+        else:
+            self.epoch += 1
+            poison = [p + 4 * _POISON for p in self.fptrs]
+            for op in merge_schedule(self.rank, self.world, lo, hi, self.epoch):
+                if op[0] == "signal":
+                    _, ph, e = op
+                    self.ctx.flag_signal_dev(self.fptrs[self.rank] + 4 * ph, e, stream=stream.cuda_stream)
+                elif op[0] == "wait":
+                    _, ph, e = op
+                    self.ctx.flag_wait_dev([p + 4 * ph for p in self.fptrs], e, self.status_ptr, self.timeout_ms,
+                                           poison_ptrs=poison, stream=stream.cuda_stream)
+                elif op[0] == "fill":
+                    _, a, b = op
+                    self.ctx.poison_fill_dev(self.ptrs[self.rank] + 8 * a, b - a, self.status_ptr,
+                                             stream=stream.cuda_stream)
+                else:
+                    self._gather(op, stream)
+        if check:
+            self.check(stream)
         return self.words
 
     def _gather(self, op, stream):
         if op[0] == "gather":
             _, a, b, srcs = op
             self.ctx.or_gather_dev(self.ptrs[self.rank] + 8 * a, [self.ptrs[r] + 8 * a for r in srcs], b - a,
-                                   stream=stream.cuda_stream)
+                                   stream=stream.cuda_stream, status_ptr=self.status_ptr)
         else:  # "copy": every other rank's merged slice in one kernel
             _, lo, hi, per, srcs = op
             ptrs = [self.ptrs[r] + 8 * lo if r in srcs else 0 for r in range(self.world)]
-            self.ctx.copy_slices_dev(self.ptrs[self.rank] + 8 * lo, ptrs, per, hi - lo, stream=stream.cuda_stream)
+            self.ctx.copy_slices_dev(self.ptrs[self.rank] + 8 * lo, ptrs, per, hi - lo, stream=stream.cuda_stream,
+                                     status_ptr=self.status_ptr)
 
 
 def merge_schedule(rank, world, lo, hi, epoch):
     """The device-ordered merge of words[lo:hi] as this rank's stream sees it,
     in order: ("signal", phase, epoch) — set my flag[phase] = epoch;
-    ("wait", phase, epoch) — until every rank's flag[phase] >= epoch;
+    ("wait", phase, epoch) — until every rank's flag[phase] >= epoch (a
+    timeout, or any rank's poison word set, poisons this merge instead);
     ("gather", a, b, ranks) — my words[a:b] = OR of those ranks' words[a:b]
     (my own index among them: in place); ("copy", lo, hi, per, ranks) — for
     each listed rank r, my words of slice r (words [lo + r per, lo + (r+1) per)
     within [lo, hi)) = rank r's (lsmb_copy_slices_dev: one kernel, every peer
-    link at once).  Phase 0: every partial of the range is final; 1: every
-    slice merged; 2: every rank holds the merged range."""
+    link at once); ("fill", lo, hi) — my words[lo:hi] = all-ones if this merge
+    is poisoned.  A poisoned gather / copy writes all-ones and reads no peer.
+    Phase 0: every partial of the range is final; 1: every slice merged; 2:
+    every rank holds the merged range."""
     per = _slices(hi - lo, world)
     sl = [(min(hi, lo + r * per), min(hi, lo + (r + 1) * per)) for r in range(world)]
     ops = [("signal", 0, epoch), ("wait", 0, epoch)]
@@ -246,4 +300,6 @@ def merge_schedule(rank, world, lo, hi, epoch):
     if peers:
         ops.append(("copy", lo, hi, per, peers))
     ops += [("signal", 2, epoch), ("wait", 2, epoch)]
+    if hi > lo:
+        ops.append(("fill", lo, hi))
     return ops

@@ -73,3 +73,35 @@ def test_compact_line_fits_the_driver_tail():
     assert c["legs"]["c5_shard"]["words_equal_oracle_fixture"] is True
     assert c["legs"]["c3_probe"]["ms"] == full["probe"]["ms"]
     assert c["legs"]["c3_probe"]["answers_equal_oracle_fixture"] is True
+
+
+def test_invalid_reasons():
+    """VERDICT r05 item 1 / ADVICE r05: a line whose own checks fail publishes no
+    number — bench.invalid_reasons lists why, main() then sets value null and
+    exits non-zero (the GPU test test_bench_fault_nulls_the_value runs it)."""
+    assert bench.invalid_reasons({"words_equal_oracle_fixture": True}) == []
+    assert bench.invalid_reasons({"words_equal_oracle_fixture": None}) == []  # no fixture for this config
+    r = bench.invalid_reasons({"words_equal_oracle_fixture": False, "multi_gpu_merged_equals_single_gpu_build": False})
+    assert len(r) == 2
+    assert bench.invalid_reasons({"multi_gpu_check_error": "x"}) == ["multi_gpu_check_error"]
+    ss = {"step_split": {"flag_timeouts": 2, "merge_poisoned": True}}
+    assert bench.invalid_reasons(ss, timed_merge="ipc") and not bench.invalid_reasons(ss, timed_merge="rccl")
+    assert bench.invalid_reasons({"step_split": {"flag_timeouts": 0, "merge_poisoned": True}}, timed_merge="ipc")
+
+
+def test_compact_line_carries_c5_full_and_invalid():
+    """the N = 1 line carries legs.c5_full (all 1e9 C5 keys on
+    one GPU: the N > 1 curve's same-workload point) within the line budget; an
+    invalid line carries its reasons."""
+    import json
+    full = json.loads(open(os.path.join(ROOT, "profiles", "r05", "r05r_bench_detail.json")).read())
+    full["detail"] = "gpurun_out/bench_detail.json"
+    full["c5_full"] = {"value": 34000.0, "ms": 29.4, "kernel_ms": 29.4, "sweeps": 2, "words_equal_oracle_fixture": True,
+                       "roofline": bench.leg_roofline(None, 16 * 10 ** 9 + 8 * 67108864, 29.4, "build")}
+    full["invalid"] = ["words_equal_oracle_fixture is false"]
+    line = json.dumps(bench.compact_line(full), separators=(",", ":"))
+    assert len(line) < bench.LINE_BUDGET, len(line)
+    c = json.loads(line)
+    assert c["legs"]["c5_full"]["words_equal_oracle_fixture"] is True and c["legs"]["c5_full"]["sweeps"] == 2
+    assert c["legs"]["c5_full"]["roofline"]["frac"] > 0
+    assert c["invalid"] == full["invalid"]

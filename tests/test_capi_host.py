@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol():
     for name in sorted(declared):
         assert hasattr(L, name), name
     assert declared == set(lsmbloom.SIGNATURES), declared ^ set(lsmbloom.SIGNATURES)
-    assert L.lsmb_abi_version() == 5
+    assert L.lsmb_abi_version() == 6
 
 
 def test_params_match_golden_sizing():
