@@ -17,7 +17,8 @@ __device__ __forceinline__ uint32_t rnd(uint32_t& s) {
 
 // MODE 0: ds_add_rtn_u32 over NB counters; 1: ds_add_u32 (no return);
 // 2: ds_or_b64 over NB*8 words; 3: ds_write_b32 over NB*16 words;
-// 4: ds_or_b32 over 32768 words (pass B); 5: ds_read_b32 random over NB counters
+// 4: ds_or_b32 over 32768 words (pass B); 5: ds_read_b32 random over NB counters;
+// 7 / 8: mode 4 with ~1/2 / ~1/4 of the lanes active (exec-masked)
 template <int MODE>
 __global__ __launch_bounds__(1024) void k(uint32_t nb, uint32_t* out) {
     extern __shared__ uint32_t lds[];
@@ -35,6 +36,10 @@ __global__ __launch_bounds__(1024) void k(uint32_t nb, uint32_t* out) {
         if (MODE == 3) lds[r & (16 * nb - 1)] = r;
         if (MODE == 4) atomicOr(&lds[r & 32767], 1u << (r >> 27));
         if (MODE == 5) acc += lds[r & m];
+        // round 6: does a half-masked ds_or cost half?  (k_apply<21>'s halves
+        // each issue every offset's ds_or with ~half of the lanes active)
+        if (MODE == 7 && ((r >> 26) & 1)) atomicOr(&lds[r & 32767], 1u << (r >> 27));
+        if (MODE == 8 && ((r >> 25) & 3) == 0) atomicOr(&lds[r & 32767], 1u << (r >> 27));
     }
     __syncthreads();
     out[blockIdx.x * 1024 + threadIdx.x] = acc + lds[threadIdx.x % words];
@@ -71,5 +76,7 @@ int main() {
     run(k<4>, "ds_or_b32 random / 32768 words", 32768 * 4);
     run(k<5>, "ds_read_b32 random / 1024 ctr", 1024 * 4);
     run(k<6>, "VALU only (xorshift)", 1024 * 4);
+    run(k<7>, "ds_or_b32 / 32768 words, 1/2 lanes active", 32768 * 4);
+    run(k<8>, "ds_or_b32 / 32768 words, 1/4 lanes active", 32768 * 4);
     return 0;
 }
