@@ -972,7 +972,7 @@ def bench_c5_full(ctx, dev, reps=4):
                        "(lsmb_build_fixed_dev_sweep_new, as each rank at N > 1)" % (n, nb, k, nsw),
            "value": round(n / (ms * 1e-3) / 1e6, 1), "unit": "Mkeys/s", "ms": round(ms, 3), "kernel_ms": round(ms, 3),
            "sweeps": nsw, "strategy": lsmbloom.build_strategy(nb, n, k),
-           "roofline": leg_roofline(None, alg, ms, "build (%d sweeps of k_bin + k_apply<21> + k_ovf_apply)" % nsw)}
+           "roofline": leg_roofline("c5_full", alg, ms, "build (%d sweeps of k_bin + k_apply<21> + k_ovf_apply)" % nsw)}
     res["words_equal_oracle_fixture"] = fixture_check(w, "c5", nb)
     del w, keys
     return res

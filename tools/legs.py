@@ -7,6 +7,8 @@ kernels after the setup, so a pass's per-kernel means belong to this leg.
   c2        C2: 100 M 16-B keys into new(1e8, 0.01), lsmb_build_fixed_dev_new
   exact10   the C2 keys into num_bits = 1e9, k = 7
   c5        C5 shard: 125 M keys into new(1e9, 0.01) = 2^32-1 bits (2 sweeps)
+  c5_full   C5 on one GPU: all 1e9 keys into the same filter, sweep by sweep
+            (lsmb_build_fixed_dev_sweep_new, as each rank builds at N > 1)
   c4        C4: 100 M var-len keys (8-256 B) into new(1e8, 0.01), lsmb_build_var_dev_new
   probe     C3: 10 M keys x 8 new(1000, 0.01) filters, lsmb_probe_dev
   fset      the same through the device filter set (range pre-check + bloom)
@@ -24,7 +26,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 import bench  # noqa: E402  (the legs' shared setup: ProbeLegs, seeds)
 
-LEGS = ("c2", "exact10", "c5", "c4", "probe", "fset", "fset_mixed", "fset_rows1")
+LEGS = ("c2", "exact10", "c5", "c5_full", "c4", "probe", "fset", "fset_mixed", "fset_rows1")
 
 
 def main():
@@ -53,6 +55,17 @@ def main():
 
         def run():
             ctx.build_fixed_dev_new(keys, 16, n, nb, k, words)
+    elif leg == "c5_full":
+        n = 1_000_000_000
+        nb, k = lsmbloom.params(n, 0.01)
+        keys = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+        ctx.gen_key16_dev(bench.SEED_MEMBERS, 0, n, keys)
+        words = torch.empty(lsmbloom.num_words(nb), dtype=torch.int64, device=dev)
+        nsw = lsmbloom.build_sweeps(nb, n, k)
+
+        def run():
+            for s in range(nsw):
+                ctx.build_fixed_dev_sweep_new(keys, 16, n, nb, k, words, s)
     elif leg == "c4":
         n = 100_000_000
         data, offs = ctx.gen_varlen_dev(n, device=dev)

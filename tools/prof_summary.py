@@ -113,6 +113,7 @@ LEG_KERNELS = {
     "c2": ("k_bin", "k_apply", "k_ovf_apply"),
     "exact10": ("k_bin", "k_apply", "k_ovf_apply"),
     "c5": ("k_bin", "k_apply", "k_ovf_apply"),
+    "c5_full": ("k_bin", "k_apply", "k_ovf_apply"),
     "c4": ("k_hash_var", "k_bin", "k_apply", "k_ovf_apply"),
     "probe": ("k_probe_sliced",),
     "fset": ("k_fset_sliced",),

@@ -8,7 +8,7 @@
 # Usage: tools/profile_legs.sh <tag> [legs...]
 set -uo pipefail
 TAG=${1:-r04}; shift || true
-LEGS=${*:-c2 exact10 c5 c4 probe fset fset_mixed fset_rows1}
+LEGS=${*:-c2 exact10 c5 c5_full c4 probe fset fset_mixed fset_rows1}
 REPO=${GRAFT_REPO_ROOT:-/root/repo}
 OUT=$REPO/gpurun_out/legs_$TAG
 mkdir -p "$OUT"
