@@ -53,10 +53,11 @@ def test_compact_line_fits_the_driver_tail():
     """VERDICT r04 "missing" item 2: the driver keeps ~8 KB of output, so the
     one JSON line must carry every leg (the C3 probe half of the metric
     included) within LINE_BUDGET bytes.  Checked on the committed full record
-    of a round-5 run (profiles/r05/r05r_bench_detail.json, every leg present,
-    the C5 shard and the one-byte filter-set rows included)."""
+    of a round-6 run (profiles/r06/r06a_bench_detail.json, every leg present:
+    the C5 shard, the 1-GPU C5 point and the one-byte filter-set rows
+    included)."""
     import json
-    full = json.loads(open(os.path.join(ROOT, "profiles", "r05", "r05r_bench_detail.json")).read())
+    full = json.loads(open(os.path.join(ROOT, "profiles", "r06", "r06a_bench_detail.json")).read())
     full["detail"] = "gpurun_out/bench_detail.json"
     line = json.dumps(bench.compact_line(full), separators=(",", ":"))
     assert len(line) < bench.LINE_BUDGET
@@ -69,8 +70,13 @@ def test_compact_line_fits_the_driver_tail():
     for k in ("value", "unit", "cores", "kind", "sample"):
         assert k in c["cpu_baseline"], k
     assert set(c["legs"]) >= {"c3_probe", "fset", "fset_mixed", "fset_rows1", "c2_exact10", "c4", "c5_shard",
-                              "c1_gpu", "e2e"}
+                              "c5_full", "c1_gpu", "e2e"}
     assert c["legs"]["c5_shard"]["words_equal_oracle_fixture"] is True
+    # the N > 1 curve's same-workload 1-GPU point
+    c5f = c["legs"]["c5_full"]
+    assert c5f["words_equal_oracle_fixture"] is True and c5f["sweeps"] == 2 and c5f["ms"] > 0
+    assert c5f["roofline"]["frac"] > 0 and c5f["value"] > 0
+    assert "invalid" not in c and c["value"] > 0
     assert c["legs"]["c3_probe"]["ms"] == full["probe"]["ms"]
     assert c["legs"]["c3_probe"]["answers_equal_oracle_fixture"] is True
 
