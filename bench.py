@@ -1175,22 +1175,21 @@ def committed_legs():
 # LDS: SQ_LDS_IDX_ACTIVE = LDS-array cycles over the 256 CUs' LDS.
 VALU_CYCLES_PER_INST = 4.0
 SATURATED = 0.75  # a unit busier than this fraction of the launch's cycles is its limiter
-# The C2 compute floor, re-measured on the round-5 arithmetic (tools/mb_hash.hip,
-# profiles/r05/r05a_hash_floor.log): XXH3-128 of 100 M 16-B keys + their 7 exact
-# positions, k = 7 unrolled, at full occupancy; the same at pass A's geometry
-# (1024-thread workgroups, one per CU), and with pass A's claims and ring slot
-# writes added (no flush, no barriers).
-HASH_WALK_FLOOR = {"ms": 0.354, "pass_a_geometry_ms": 0.404, "with_claims_and_slot_writes_ms": 0.538,
-                   "source": "profiles/r05/r05a_hash_floor.log",
+# The C2 compute floor (tools/mb_hash.hip, profiles/r06/r06c_hash_floor.log): XXH3-128
+# of 100 M 16-B keys + their 7 exact positions, k = 7 unrolled, at full
+# occupancy; the same at pass A's geometry (1024-thread workgroups, one per CU),
+# and with pass A's claims and ring slot writes added (no flush, no barriers).
+HASH_WALK_FLOOR = {"ms": 0.363, "pass_a_geometry_ms": 0.428, "with_claims_and_slot_writes_ms": 0.558,
+                   "source": "profiles/r06/r06c_hash_floor.log",
                    "what": "no build can beat the hash + position arithmetic alone"}
-# Where pass A's phase goes (LSMB_STAMP build, profiles/r05/r05e_stamps.log;
+# Where pass A's phase goes (LSMB_STAMP build, profiles/r06/r06c_stamps.log;
 # shares of the cycles per phase per wave) and the ablations around it
-# (tools/build_variants.sh + run_variants.sh, profiles/r05/r05e_passA_ablations.log:
+# (tools/build_variants.sh + run_variants.sh, profiles/r06/r06c_passA_ablations.log:
 # pass A ms with no flush / no region stores / every region store dropped).
-PASS_A_PHASE = {"cycles": 6228, "work": 0.356, "barrier1": 0.169, "flush": 0.322, "barrier2": 0.152,
-                "ablation_pass_a_ms": {"product": 0.980, "no_flush": 0.570, "no_region_stores": 0.733,
-                                       "stores_dropped": 0.857},
-                "source": "profiles/r05/r05e_stamps.log, r05e_passA_ablations.log"}
+PASS_A_PHASE = {"cycles": 6241, "work": 0.356, "barrier1": 0.170, "flush": 0.321, "barrier2": 0.154,
+                "ablation_pass_a_ms": {"product": 0.982, "no_flush": 0.582, "no_region_stores": 0.739,
+                                       "stores_dropped": 0.864},
+                "source": "profiles/r06/r06c_stamps.log, r06c_passA_ablations.log"}
 
 
 def native_record():
