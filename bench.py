@@ -52,6 +52,7 @@ def parse():
                     help="let auto run with more ranks than visible GPUs (as ipc: a one-GPU rehearsal; the line then "
                          "says ranks_per_gpu > 1 and is not a scaling figure)")
     ap.add_argument("--inject-merge-fault", action="store_true", help=argparse.SUPPRESS)  # tests: a wrong merge
+    ap.add_argument("--inject-ipc-poison", action="store_true", help=argparse.SUPPRESS)  # tests: IPC merge poisoned
     ap.add_argument("--probe-keys", type=int, default=10_000_000)
     ap.add_argument("--probe-filters", type=int, default=8)
     ap.add_argument("--no-probe", action="store_true")
@@ -400,6 +401,11 @@ def main():
         # signalled (or its flags are not visible here); the merge is then
         # dropped below instead of stalling every step.
         ipc.timeout_ms = 3000
+        if args.inject_ipc_poison and rank == world - 1:
+            # tests: this rank's merge status starts poisoned, as after a peer
+            # timed out on it; every rank's IPC merge then ends all-ones
+            ipc.flags[3] = 1
+            torch.cuda.synchronize(dev)
     if world > 1 and len(merges) > 1:
         # The merges must agree word for word (one serial step each, untimed,
         # before any warm-up) and the IPC merge's waits must all have been

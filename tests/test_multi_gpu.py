@@ -418,6 +418,29 @@ def test_bench_fault_nulls_the_value():
     assert any("multi_gpu_merged_equals_single_gpu_build" in x for x in out["invalid"])
 
 
+@pytest.mark.timeout(300)
+def test_bench_auto_drops_a_poisoned_ipc_merge():
+    """--backend auto's agreement step with an IPC merge that fails safe: the
+    last rank's merge status starts poisoned (--inject-ipc-poison), so every
+    rank's IPC merge ends all-ones instead of exact.  The merges then disagree,
+    IPC is dropped before any timing, the other merge (gloo here, RCCL on a
+    multi-GPU node) is the one timed, and the line stands: its merged filter
+    passes the word check."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "auto-gloo",
+           "--global-keys", "2000000", "--filter-keys", "1000000000", "--steps", "2", "--warmup", "1",
+           "--no-cpu-baseline", "--no-e2e", "--no-varlen", "--no-exact10", "--no-probe", "--inject-ipc-poison"]
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    out = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])
+    ss = out["step_split"]
+    assert ss["merges_agree"] is False and "ipc" not in ss["merges_available"] and ss["merge"] == "gloo"
+    assert ss["merge_poisoned"] is True  # reported, though not the timed merge
+    assert out["multi_gpu_merged_equals_single_gpu_build"] is True
+    assert "invalid" not in out and out["value"] > 0
+
+
 def test_bench_auto_refuses_ranks_sharing_a_gpu():
     """--backend auto (the default) with more ranks than visible GPUs
     exits 2, as nccl does, instead of timing N ranks on fewer GPUs."""
