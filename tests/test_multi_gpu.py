@@ -558,10 +558,13 @@ def a_stream(c):
     return 0
 
 
-def _silent_rank_worker(rank, port, n, filter_n, q):
+def _silent_rank_worker(rank, port, n, filter_n, q, late=False):
     """World 2 on cuda:0: both ranks build their shard; rank 1 then agrees on
     the word range and never runs its merge kernels (a rank that died after
-    the range check), rank 0 merges device-ordered with a short timeout."""
+    the range check), rank 0 merges device-ordered with a short timeout.
+    late=True: rank 1 is alive but stalls past the timeout, then merges: its
+    waits must see rank 0's poison (published across processes) and its own
+    merge must end all-ones and raise too."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     sys.path.insert(0, os.path.join(ROOT, "storage-engine_amd"))
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -583,7 +586,10 @@ def _silent_rank_worker(rank, port, n, filter_n, q):
         ctx.build_fixed_dev_new(keys, 16, hi - lo, nb, k, words)
         torch.cuda.synchronize()
         raised = None
-        if rank == 0:
+        if rank == 0 or late:
+            if rank == 1:
+                m._check_range(0, words.numel())  # the range collective, then the stall
+                time.sleep(1.5)
             t0 = time.time()
             try:
                 m.allreduce(check=True)
@@ -629,6 +635,32 @@ def test_ipc_merge_with_a_silent_rank_fails_safe(oracle):
     ref = oracle.build_fixed_mt(keygen.key16(0x5EED0001, 0, n), 16, nb, k, 8)
     assert ref.any() and digest != _digest(ref)  # all-ones: every oracle bit set, and more
     assert elapsed < 30  # a poisoned merge does not wait out every phase
+
+
+@pytest.mark.timeout(240)
+def test_ipc_merge_with_a_late_rank_fails_safe():
+    """The stalled (not dead) peer on the GPU: rank 1 merges 1.5 s late, past
+    rank 0's 300 ms timeout.  Rank 0 gives up and poisons; rank 1's first wait
+    then finds rank 0's flags already set but reads its poison word through the
+    IPC mapping, so it poisons itself without reading rank 0's (possibly
+    rewritten) words: both ranks end all-ones, with no timeout on rank 1, and
+    both raise MergePoisoned."""
+    import torch.multiprocessing as mp
+    mpc = mp.get_context("spawn")
+    q = mpc.Queue()
+    port = _free_port()
+    procs = [mpc.Process(target=_silent_rank_worker, args=(r, port, 2_000_000, 20_000_000, q, True)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=200) for _ in range(2)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, digest, all_ones, raised, poisoned, tmo, elapsed in res:
+        assert raised and "poisoned" in raised, rank
+        assert poisoned and all_ones, rank
+    assert res[0][5] >= 1  # rank 0 timed out waiting for rank 1
+    assert res[1][5] == 0 and res[1][6] < 5  # rank 1 saw the poison at once
 
 
 def test_merge_status_kernels(torch, ctx):
