@@ -70,6 +70,8 @@ def parse():
     ap.add_argument("--no-c1", action="store_true", help="skip the C1-on-the-GPU leg")
     ap.add_argument("--no-overlap", action="store_true",
                     help="N > 1: build the whole filter, then OR-allreduce it (no per-sweep overlap)")
+    ap.add_argument("--step-form", default="auto", choices=("auto", "overlapped", "pipelined", "serial"),
+                    help="N > 1: the step form to time (auto: the fastest of the calibration)")
     ap.add_argument("--varlen-keys", type=int, default=100_000_000)
     ap.add_argument("--filter-keys", type=int, default=0, help="size the filter for this many keys (default: the global run)")
     ap.add_argument("--detail-out", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
@@ -363,24 +365,45 @@ def main():
     overlap = world > 1 and nsw > 1 and not args.no_overlap
     side = torch.cuda.Stream(dev) if overlap else None
     sweep_ev = [torch.cuda.Event() for _ in range(nsw)]
+    merge_ev = [torch.cuda.Event() for _ in range(nsw)]
+    pending = [False] * nsw  # pipelined steps: range s's last merge may still run on `side`
+    # Step forms: "serial" (build, then merge the whole filter), "overlapped"
+    # (range s merges on a side stream while sweep s+1 builds; the step ends
+    # when every merge has), "pipelined" (the same, and the step does not wait
+    # for its last range's merge: the next step's sweep 0, which rewrites only
+    # range 0, runs under it, and sweep s waits only for range s's previous
+    # merge — back-to-back flushes / compactions as a stream).  Every form's
+    # work is inside the timed region, which ends with a device synchronise.
+    mode = "overlapped" if overlap else "serial"
 
     def allreduce(f=None):
         if world > 1:
             merges[f or form](0, nw, torch.cuda.current_stream(dev))
 
-    def step(ov=None, f=None):
+    def step(md=None, f=None):
         f = f or form
-        if not (overlap if ov is None else ov):
+        md = md or mode
+        main = torch.cuda.current_stream(dev)
+        if md == "serial":
+            if side is not None and any(pending):  # a full rewrite waits for pipelined merges
+                main.wait_stream(side)
+                pending[:] = [False] * nsw
             build()
             allreduce(f)
             return
-        main = torch.cuda.current_stream(dev)
         for s, (a, b) in enumerate(ranges):
+            if pending[s]:
+                main.wait_event(merge_ev[s])  # range s's previous merge is done with these words
             ctx.build_fixed_dev_sweep_new(keys, 16, npg, nb, k, words, s)
             sweep_ev[s].record(main)
             side.wait_event(sweep_ev[s])
             merges[f](a, b, side)
-        main.wait_stream(side)
+            if md == "pipelined":
+                merge_ev[s].record(side)
+                pending[s] = True
+        if md != "pipelined":
+            main.wait_stream(side)
+            pending[:] = [False] * nsw
 
     def barrier():
         if world > 1:
@@ -413,7 +436,7 @@ def main():
         snaps, failed = {}, None
         for f in merges:
             try:
-                step(False, f)
+                step("serial", f)
                 torch.cuda.synchronize(dev)
             except Exception as e:  # an IPC merge error drops IPC (its waits time out on the peers)
                 if f != "ipc":
@@ -435,29 +458,34 @@ def main():
         if not merge_notes["merges_agree"]:
             merges.pop("ipc", None)
             form = next(iter(merges))
-    forms = [(f, ov) for f in (merges or [None]) for ov in ((True, False) if overlap else (False,))]
+    modes = ("overlapped", "pipelined", "serial") if overlap else ("serial",)
+    if args.step_form != "auto" and overlap:
+        modes = (args.step_form,)
+        mode = args.step_form
+    forms = [(f, md) for f in (merges or [None]) for md in modes]
     for i in range(args.warmup):
         step(forms[i % len(forms)][1], forms[i % len(forms)][0])
     barrier()
     if len(forms) > 1:
-        # Overlapped vs serial and RCCL vs IPC: the overlapped collective shares
-        # the CUs with pass A, whose workgroups each need a whole CU's LDS, and
-        # the merges' speed depends on the node's links.  Time a few steps of
-        # each form (untimed for the metric; the max over ranks, so every rank
-        # picks the same) and time the fastest.
-        def timed(f, ov, reps):
+        # Overlapped / pipelined vs serial and RCCL vs IPC: the overlapped
+        # collective shares the CUs with pass A, whose workgroups each need a
+        # whole CU's LDS, and the merges' speed depends on the node's links.
+        # Time a few steps of each form (untimed for the metric; the max over
+        # ranks, so every rank picks the same) and time the fastest.
+        def timed(f, md, reps):
             barrier()
             t = time.perf_counter()
             for _ in range(reps):
-                step(ov, f)
+                step(md, f)
             barrier()
             return max_over_ranks(time.perf_counter() - t) / reps * 1e3
         reps = max(2, min(5, args.steps))
-        cal = {(f, ov): timed(f, ov, reps) for f, ov in forms}
-        form, overlap = min(cal, key=cal.get)
-        calib = {"%s_%s_ms_per_step" % (f, "overlapped" if ov else "serial"): round(v, 4)
-                 for (f, ov), v in cal.items()}
-        calib.update({"steps_each": reps, "timed_form": "overlapped" if overlap else "serial", "timed_merge": form})
+        cal = {(f, md): timed(f, md, reps) for f, md in forms}
+        form, mode = min(cal, key=cal.get)
+        calib = {"%s_%s_ms_per_step" % (f, md): round(v, 4) for (f, md), v in cal.items()}
+        calib.update({"steps_each": reps, "timed_form": mode, "timed_merge": form})
+    if args.step_form != "auto" and overlap:
+        calib = dict(calib or {}, timed_form=mode, timed_merge=form, step_form="forced by --step-form")
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -536,9 +564,12 @@ def main():
                                      "bitwise-OR allreduce of the whole filter (%s)" % merge_what.get(form, form),
                              "serial_ms_per_step": round(serial_ms, 4),
                              "overlap_calibration": calib,
-                             "timed_step": ("%d build sweeps, each sweep's word range OR-allreduced on a side "
-                                            "stream while the next sweep builds" % nsw) if overlap
-                                           else "build then OR-allreduce",
+                             "timed_step": {"overlapped": "%d build sweeps, each sweep's word range OR-allreduced on "
+                                                          "a side stream while the next sweep builds" % nsw,
+                                            "pipelined": "%d build sweeps, each sweep's word range OR-allreduced on "
+                                                         "a side stream while the next sweep builds, the last one "
+                                                         "while the next step's first sweep builds" % nsw,
+                                            "serial": "build then OR-allreduce"}[mode],
                              "merge": form,
                              "merges_available": list(merges),
                              "or_allreduce_bytes_per_gpu": int(moved),

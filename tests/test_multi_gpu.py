@@ -356,6 +356,27 @@ def test_ipc_or_allreduce_cross_process(oracle, world, n, filter_n, per_sweep, o
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("backend", ["gloo", "ipc"])
+def test_bench_pipelined_steps(backend):
+    """The pipelined step form (--step-form pipelined): a step does not wait for
+    its last range's merge, the next step's sweep 0 (range 0 only) runs under
+    it and sweep s waits only for range s's previous merge.  After the timed
+    steps the merged filter must still equal the single-GPU build, word for
+    word, with either merge."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", backend,
+           "--global-keys", "8000000", "--filter-keys", "1000000000", "--steps", "4", "--warmup", "2",
+           "--step-form", "pipelined", "--no-cpu-baseline", "--no-e2e", "--no-varlen", "--no-exact10", "--no-probe"]
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    out = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])
+    assert "the last one while the next step's first sweep builds" in out["step_split"]["timed_step"]
+    assert out["step_split"]["overlap_calibration"]["timed_form"] == "pipelined"
+    assert out["multi_gpu_merged_equals_single_gpu_build"] is True and out["value"] > 0
+
+
+@pytest.mark.timeout(300)
 @pytest.mark.parametrize("filter_keys,backend", [(None, "gloo"), (1_000_000_000, "gloo"), (1_000_000_000, "ipc"),
                                                  (1_000_000_000, "auto-gloo")])
 def test_bench_launches_its_own_ranks(filter_keys, backend):
@@ -383,9 +404,10 @@ def test_bench_launches_its_own_ranks(filter_keys, backend):
         merges = out["step_split"]["merges_available"]
         assert set(merges) == ({"gloo", "ipc"} if backend == "auto-gloo" else {backend})
         for m in merges:
-            assert cal["%s_overlapped_ms_per_step" % m] > 0 and cal["%s_serial_ms_per_step" % m] > 0
+            for md in ("overlapped", "pipelined", "serial"):
+                assert cal["%s_%s_ms_per_step" % (m, md)] > 0
         assert cal["timed_merge"] == out["step_split"]["merge"] in merges
-        assert out["step_split"]["timed_step"].startswith("2 build sweeps") == (cal["timed_form"] == "overlapped")
+        assert out["step_split"]["timed_step"].startswith("2 build sweeps") == (cal["timed_form"] != "serial")
         if backend == "auto-gloo":  # both merges ran, agreed word for word, the faster was timed
             assert out["step_split"]["merges_agree"] is True
         if "ipc" in merges:
