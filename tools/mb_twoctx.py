@@ -24,6 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--n", type=int, default=100_000_000)
+    ap.add_argument("--lags", type=int, nargs="*", default=[50_000, 100_000, 200_000, 400_000, 800_000])
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     n = args.n
@@ -42,10 +43,13 @@ def main():
     torch.cuda.synchronize()
     streams = [torch.cuda.Stream(dev) for _ in range(2)]
 
-    def run(mode, reps):
+    def run(mode, reps, lag=0):
         torch.cuda.synchronize()
         t = time.perf_counter()
         builds = 0
+        if lag:  # stream 1 starts `lag` clock cycles after stream 0 (phase offset)
+            with torch.cuda.stream(streams[1]):
+                torch.cuda._sleep(lag)
         for r in range(reps):
             if mode == "one":
                 ctxs[0].build_fixed_dev_new(keys[r & 1], 16, n, nb, k, words[r & 1], stream=streams[0].cuda_stream)
@@ -57,11 +61,15 @@ def main():
         torch.cuda.synchronize()
         return (time.perf_counter() - t) * 1e3 / builds, builds
 
-    for mode in ("one", "two", "one", "two"):
-        run(mode, 3)
-        ms, b = run(mode, args.reps)
+    t = time.perf_counter()
+    torch.cuda._sleep(1_000_000)
+    torch.cuda.synchronize()
+    print(json.dumps({"sleep_1e6_cycles_ms": round((time.perf_counter() - t) * 1e3, 3)}), flush=True)
+    for mode, lag in [("one", 0), ("two", 0)] + [("two", x) for x in args.lags] + [("one", 0)]:
+        run(mode, 3, lag)
+        ms, b = run(mode, args.reps, lag)
         exact = all(torch.equal(words[i], ref[i]) for i in range(2))
-        print(json.dumps({"mode": mode, "builds": b, "ms_per_build": round(ms, 4),
+        print(json.dumps({"mode": mode, "lag_cycles": lag, "builds": b, "ms_per_build": round(ms, 4),
                           "Mkeys_s": round(n / ms / 1e3, 1), "words_exact": exact}), flush=True)
         if not exact:
             return 1
