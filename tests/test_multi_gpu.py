@@ -423,6 +423,41 @@ def torch_count():
 
 
 @pytest.mark.timeout(300)
+def test_bench_under_torch_distributed_run():
+    """The driver's N > 1 launch: `python -m torch.distributed.run --nnodes=1
+    --nproc-per-node 2 --master-addr 127.0.0.1 --master-port P bench.py --gpus
+    2 ...`, the ranks from the launcher's environment (RANK / LOCAL_RANK /
+    WORLD_SIZE), not self-started.  Both ranks share this box's one GPU, so the
+    merge is the IPC one (the default `auto` needs one GPU per rank: checked
+    below to refuse with exit 2 and no line); rank 0 alone prints the line."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    base = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2",
+            "--global-keys", "8000000", "--filter-keys", "1000000000", "--steps", "3", "--warmup", "2",
+            "--no-cpu-baseline", "--no-e2e", "--no-varlen", "--no-exact10", "--no-probe"]
+    env = dict(os.environ)
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(v, None)
+    r = subprocess.run(base + ["--backend", "ipc"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["step_split"]["merge"] == "ipc"
+    assert out["multi_gpu_merged_equals_single_gpu_build"] is True and out["value"] > 0
+    assert out["config"]["ranks_per_gpu"] == (2 if torch_count() < 2 else 1)
+    if torch_count() < 2:
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            base[base.index("--master-port") + 1] = str(s.getsockname()[1])
+        r = subprocess.run(base, capture_output=True, text=True, timeout=300, env=env)
+        assert r.returncode != 0 and not [x for x in r.stdout.splitlines() if x.startswith("{")], r.stdout[-2000:]
+
+
+@pytest.mark.timeout(300)
 def test_bench_fault_nulls_the_value():
     """at N > 1 a merged filter that fails its own word
     check (here a bit flipped on rank 0 after the self-check step,
