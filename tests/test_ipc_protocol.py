@@ -9,7 +9,9 @@ overlaps a live write) is a race.  Random delays widen every window.
 Checked: no race, and after each merge every rank holds the OR of all ranks'
 partials of that build, across consecutive builds (the overlapped N > 1 step
 of bench.py, which rebuilds the words right after a merge).  The negative
-controls drop one wait from the schedule and must be caught.
+controls drop one wait from the schedule and must be caught.  run_streams plays
+the overlapped and pipelined step forms with two streams per rank (a build
+stream rewriting one sweep's range while the side stream merges another).
 
 The fail-safe: with a short timeout, a rank that dies
 after its build, or stalls past the timeout, must never make a live rank end
@@ -330,3 +332,128 @@ def test_failsafe_checker_catches_a_missing_poison_check():
         Sim.gather, Sim.fill = orig, orig_fill
     want = _want(partials, 0, world)
     assert any(not ((snaps[r][0] & want) == want).all() for r in (0, 1))
+
+
+def _build_range(sim, me, values, lo, hi, scale):
+    """A fresh sweep: rewrites my words[lo:hi] (its own range and nothing else)."""
+    rec = sim._enter(me, lo, hi, True, me)
+    try:
+        sim.pause(scale)
+        sim.words[me][lo:hi] = values
+        sim.pause(scale)
+    finally:
+        sim._leave(rec)
+
+
+def run_streams(world, nwords, ranges, builds, seed, form, skip_merge_wait=False):
+    """bench.py's N > 1 step forms with two streams per rank, one thread each:
+    the build stream runs sweep s of build b (rewriting range s only), the
+    side stream merges range s once that sweep is done (merge_schedule, epochs
+    in merge order).  Before sweep s of build b+1 the build stream waits for
+    range s's merge of build b ("pipelined") or for every merge of build b
+    ("overlapped": the step ends with the side stream).  Each merge snapshots
+    its range before it releases the build stream.  skip_merge_wait: the build
+    stream waits for nothing (the negative control)."""
+    sim = Sim(world, nwords, seed)
+    rng = np.random.default_rng(seed)
+    partials = [[rng.integers(0, 2 ** 63, nwords, dtype=np.uint64) & rng.integers(0, 2 ** 63, nwords, dtype=np.uint64)
+                 for _ in range(world)] for _ in range(builds)]
+    snaps = [[np.zeros(nwords, dtype=np.uint64) for _ in range(builds)] for _ in range(world)]
+
+    def rank_main(me):
+        built = [[threading.Event() for _ in ranges] for _ in range(builds)]
+        merged = [[threading.Event() for _ in ranges] for _ in range(builds)]
+        scale = 0.0015
+
+        def need(ev):
+            t0 = time.time()
+            while not ev.wait(0.01):
+                if sim.errors:  # another stream failed: stop waiting for it
+                    raise RuntimeError("aborted")
+                if time.time() - t0 > 20:
+                    raise TimeoutError("stream event never set")
+
+        def main():
+            try:
+                for bi in range(builds):
+                    for s, (lo, hi) in enumerate(ranges):
+                        if bi and not skip_merge_wait:
+                            for t in ([s] if form == "pipelined" else range(len(ranges))):
+                                need(merged[bi - 1][t])
+                        _build_range(sim, me, partials[bi][me][lo:hi], lo, hi, scale)
+                        built[bi][s].set()
+            except Exception as ex:
+                sim.errors.append(ex)
+
+        def side():
+            try:
+                epoch = 0
+                for bi in range(builds):
+                    for s, (lo, hi) in enumerate(ranges):
+                        need(built[bi][s])
+                        epoch += 1
+                        for op in merge_schedule(me, world, lo, hi, epoch):
+                            if op[0] == "signal":
+                                sim.pause(scale / 2)
+                                with sim.lock:
+                                    sim.flags[me][op[1]] = op[2]
+                            elif op[0] == "wait":
+                                sim.wait(me, op[1], op[2])
+                            elif op[0] == "gather":
+                                sim.gather(me, op[1], op[2], op[3], scale)
+                            elif op[0] == "fill":
+                                if sim.poison[me]:
+                                    sim.fill(me, op[1], op[2], scale)
+                            else:
+                                _, a, b, per, srcs = op
+                                for r in srcs:
+                                    sim.gather(me, min(b, a + r * per), min(b, a + (r + 1) * per), [r], scale)
+                        snaps[me][bi][lo:hi] = sim.words[me][lo:hi]
+                        merged[bi][s].set()
+            except Exception as ex:
+                sim.errors.append(ex)
+
+        th = [threading.Thread(target=main), threading.Thread(target=side)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(60)
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(90)
+    return sim, partials, snaps
+
+
+@pytest.mark.parametrize("world,form", [(2, "pipelined"), (3, "pipelined"), (4, "pipelined"), (3, "overlapped")])
+def test_step_forms_with_two_streams_have_no_race(world, form):
+    """The overlapped and pipelined N > 1 steps (bench.py): sweep s of the next
+    build rewrites range s while other ranges still merge on the side stream.
+    No race, and every merge leaves every rank with the exact OR of that
+    build's partials over its range."""
+    nwords = 32 * world + 6
+    ranges = [(0, nwords // 2), (nwords // 2, nwords)]
+    sim, partials, snaps = run_streams(world, nwords, ranges, builds=4, seed=40 + world, form=form)
+    assert not sim.errors, sim.errors[0]
+    assert not any(sim.poison) and not any(sim.timeouts)
+    for bi in range(4):
+        want = _want(partials, bi, world)
+        for r in range(world):
+            assert np.array_equal(snaps[r][bi], want), (form, bi, r)
+
+
+def test_step_forms_checker_catches_a_build_that_skips_the_merge_event():
+    """Negative control: a build stream that starts sweep s of the next build
+    without waiting for range s's merge rewrites words a peer may still read."""
+    world, nwords = 3, 3 * 32
+    ranges = [(0, nwords // 2), (nwords // 2, nwords)]
+    caught = 0
+    for seed in range(8):
+        sim, partials, snaps = run_streams(world, nwords, ranges, builds=3, seed=500 + seed, form="pipelined",
+                                           skip_merge_wait=True)
+        if sim.errors or any(not np.array_equal(snaps[r][bi], _want(partials, bi, world))
+                             for bi in range(3) for r in range(world)):
+            caught += 1
+    assert caught > 0
